@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Headline benchmark: gradient evals/s + ESS/s, Bayesian logistic regression N=1e8, d=100,
+fp64, 8 subposterior shards + consensus combine (BASELINE.json configs[3], the config the
+metric is quoted on; 80 GB of X fits one MI355X, so N=1 runs all 8 shards on one GPU and
+N GPUs run 8/N shards each -- total work fixed, "scaling": "strong").
+
+A "step" = one NUTS transition of every chain on every shard (each transition is
+2^depth - 1 leapfrogs, i.e. that many fused data sweeps over the shard).  Timeline:
+  data generated in HBM (Philox, not timed) -> --adapt-iters warmup transitions with Stan's
+  adaptation (not timed) -> W untimed steps -> barrier+sync -> K timed steps -> sync+barrier.
+`value` = chain-gradient evaluations of all ranks in the timed region / max-over-ranks time.
+ESS/s = min over non-lp__ parameters of the ESS of the consensus-combined timed draws
+(all-gathered over RCCL, combined on the GPU) / the same time.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--rows", type=float, default=1e8, help="total rows N over all shards")
+    p.add_argument("--d", type=int, default=100)
+    p.add_argument("--shards", type=int, default=8)
+    p.add_argument("--chains", type=int, default=4, help="chains per shard (share one data sweep)")
+    p.add_argument("--adapt-iters", type=int, default=150)
+    p.add_argument("--seed", type=int, default=20240)
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "sweep_pmc.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(d, rows_per_shard, shards, seconds):
+    """The oracle's logistic gradient (oracle/stark_oracle.c, gcc -O2, scalar) run as the
+    reference's execution model: one single-chain worker per shard, min(shards, cores)
+    concurrent (Spark local[*]).  Each worker times full gradient evaluations over a bounded
+    row sample and scales linearly to the shard (gradient cost is linear in rows)."""
+    import multiprocessing as mp
+    cores = len(os.sched_getaffinity(0))
+    workers = max(1, min(shards, cores))
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(workers) as pool:
+        rates = pool.starmap(_cpu_worker, [(d, seconds, w) for w in range(workers)])
+    sample_rows = rates[0][1]
+    per_worker_grads = [r[0] * sample_rows / rows_per_shard for r in rates]   # full-shard grads/s
+    return {"value": float(sum(per_worker_grads)), "unit": "gradient evals/sec (whole node)",
+            "cores": workers, "kind": "port",
+            "sample": f"oracle orc_logreg_lpgrad (C, 1 thread/worker) on {sample_rows} rows x d={d} per worker, "
+                      f"{seconds:.0f}s per worker, {workers} concurrent workers (one per shard, Spark local[*] model), "
+                      f"scaled linearly to {rows_per_shard:.3g} rows/shard; analytic gradient (optimistic vs Stan autodiff)"}
+
+
+def _cpu_worker(d, seconds, w):
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    rows = 100_000
+    X = O.gen_x(99, w * rows, rows, d)
+    beta = O.gen_beta(99, d)
+    y, _ = O.gen_y_logistic(99, w * rows, X, 0.0, beta)
+    m = O.Model(O.FAM_LOGREG, X=X, y=y)
+    q = np.concatenate([[0.0], beta * 0.9])
+    m.lpgrad(q)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        m.lpgrad(q)
+        n += 1
+    return n / (time.perf_counter() - t0), rows
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from stark_amd import diagnostics, engine
+
+    assert a.shards % world == 0, "shards must divide evenly over GPUs"
+    spr = a.shards // world
+    rows_per_shard = int(a.rows) // a.shards
+    first = rank * spr
+    shard_ids = list(range(first, first + spr))
+    ctx = engine.Context(local_rank)
+
+    t = time.perf_counter()
+    model = engine.Model.synthetic(ctx, "logistic", spr, rows_per_shard, a.d, data_seed=a.seed,
+                                   row_offset=first * rows_per_shard)
+    ctx.sync()
+    t_gen = time.perf_counter() - t
+
+    A, W, K = a.adapt_iters, a.warmup, a.steps
+    sampler = model.sampler(num_warmup=A, num_samples=W + K, chains=a.chains, seed=a.seed + 1,
+                            shard_ids=shard_ids)
+    t = time.perf_counter()
+    sampler.run(A)
+    t_adapt = time.perf_counter() - t
+    sampler.run(A + W)
+
+    def barrier():
+        torch.cuda.synchronize(local_rank)
+        if dist:
+            dist.barrier()
+
+    ctx.set_profiling(True)
+    i0 = sampler.info()
+    barrier()
+    t0 = time.perf_counter()
+    sampler.run(A + W + K)
+    ctx.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    i1 = sampler.info()
+
+    grads = i1["grad_evals"] - i0["grad_evals"]
+    leaps = i1["leapfrogs"] - i0["leapfrogs"]
+    sweeps = i1["sweeps"] - i0["sweeps"]
+    shard_sweeps = i1["shard_sweeps"] - i0["shard_sweeps"]
+    sweep_ms = i1["sweep_ms"] - i0["sweep_ms"]
+    if dist:
+        v = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        elapsed = float(v.item())
+        g = torch.tensor([grads, leaps], dtype=torch.float64, device="cuda")
+        dist.all_reduce(g, op=dist.ReduceOp.SUM)
+        grads, leaps = int(g[0].item()), int(g[1].item())
+
+    # ---- timed draws -> consensus combine -> ESS
+    P = model.P[0]
+    local = {}
+    for s in range(spr):
+        dr, _ = sampler.draws(s)
+        cols = np.concatenate([np.arange(c * (W + K) + W, c * (W + K) + W + K) for c in range(a.chains)])
+        local[shard_ids[s]] = np.ascontiguousarray(dr[:, cols])
+    from stark_amd import dist as sdist
+    if dist:
+        # contiguous shard blocks per rank -> gather in global shard order
+        allp = [None] * a.shards
+        gathered = [None] * world
+        dist.all_gather_object(gathered, local)
+        for dct in gathered:
+            for k_, v_ in dct.items():
+                allp[k_] = v_
+    else:
+        allp = [local[k_] for k_ in range(a.shards)]
+    ess_ps, min_ess, sub_ess = None, None, None
+    if rank == 0:
+        sub_ess = float(np.nanmin(diagnostics.ess_matrix(allp[0][:-1], a.chains)))
+        if a.chains * K > P + 1:
+            comb, used = engine.consensus(allp, ctx)
+            e = diagnostics.ess_matrix(comb[:-1], a.chains)     # drop lp__
+            min_ess = float(np.nanmin(e))
+            ess_ps = min_ess / elapsed
+    info = sampler.info()
+    sampler.close()
+
+    if rank != 0:
+        model.close()
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # ---- roofline of the dominant kernel (the data sweep)
+    bytes_per_shard = rows_per_shard * (8 * a.d + 4)        # X fp64 + y int32, once per sweep
+    avg_ms = sweep_ms / max(sweeps, 1)
+    bytes_per_launch = bytes_per_shard * shard_sweeps / max(sweeps, 1)
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if sweeps else None
+    traffic = None
+    if os.path.exists(a.traffic_json):
+        try:
+            tj = json.load(open(a.traffic_json))
+            if tj.get("rows_per_shard") == rows_per_shard and tj.get("d") == a.d and tj.get("shards_per_gpu") == spr:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+            "kernel": "k_sweep<LOGREG>", "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": bytes_per_launch}
+    cpu = None
+    if not a.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(a.d, rows_per_shard, a.shards, a.cpu_baseline_seconds)
+
+    value = grads / elapsed
+    line = {
+        "metric": "gradient evals/sec (whole node), logistic regression N=1e8 d=100",
+        "value": value,
+        "unit": "gradient evals/sec",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": 1e3 * elapsed / K,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Philox in HBM, SURVEY 8d)",
+        "config": {"workload": "bayesian logistic regression, 8 subposterior shards + consensus combine",
+                   "rows": int(a.rows), "d": a.d, "shards": a.shards, "shards_per_gpu": spr,
+                   "chains_per_shard": a.chains, "adapt_iters": A, "parallelism": f"shard-dp{world}"},
+        "ess_per_sec": ess_ps,
+        "min_ess": min_ess,
+        "subposterior_min_ess_shard0": sub_ess,
+        "leapfrogs_per_transition": leaps / max(1, a.shards * a.chains * K),
+        "rows_x_chains_per_sec": grads * rows_per_shard / elapsed,
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "setup_s": {"datagen": t_gen, "adaptation": t_adapt},
+        "divergent": info["divergent"],
+    }
+    print(json.dumps(line), flush=True)
+    model.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

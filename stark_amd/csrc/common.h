@@ -1,0 +1,91 @@
+// Internal types shared by the gfx950 kernels and the C-ABI layer of libstark_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "philox.h"
+#include "../../include/stark_hip.h"
+
+namespace stk {
+
+constexpr int WAVE = 64;
+
+// One data shard resident in HBM (copied or generated once, then streamed every sweep).
+struct ShardDev {
+  const double* x;      // n x d row-major (regressions)
+  const double* y;      // schools y / linreg y
+  const int32_t* yi;    // logreg y
+  const double* sigma;  // schools sigma
+  int64_t n;            // rows (J for schools)
+  int d;                // covariates
+  int D;                // unconstrained dimension
+  int P;                // output columns (params + transformed params + lp__)
+};
+
+// ---- per-chain NUTS state (global memory, one block of Dp-strided vectors per chain)
+enum Vec : int {
+  V_Q, V_P, V_G,        // current integration point z (g = dV/dq = -grad lp)
+  V_QF, V_PF, V_GF,     // z_plus  (forward end of the trajectory)
+  V_QB, V_PB, V_GB,     // z_minus (backward end)
+  V_QS, V_GS,           // z_sample (also the init point of init_stepsize probes)
+  V_RHO, V_PSP, V_PSM,  // trajectory rho, p_sharp at the + / - ends
+  V_IM,                 // diagonal inverse metric
+  V_WM, V_WM2,          // Welford mean / M2
+  V_COUNT
+};
+enum StackVec : int { SV_RHO, SV_PSB, SV_Q, SV_G, SV_COUNT };   // pending left subtree per level
+enum Scal : int {
+  S_V, S_VF, S_VB, S_VS, S_HS, S_H0, S_LSW, S_EPS, S_NOMEPS, S_SUMMETRO,
+  S_DA_CNT, S_SBAR, S_XBAR, S_MU, S_WFN, S_PH0, S_LFEPS, S_COUNT
+};
+enum StackScal : int { SS_LSW, SS_V, SS_H, SS_COUNT };
+enum IVar : int {
+  I_MODE, I_ITER, I_DEPTH, I_DIR, I_LEAF, I_UK, I_NLEAP, I_DIV, I_PROBE, I_PDIR,
+  I_SSCALL, I_SSREASON, I_WCNT, I_WSIZE, I_WNEXT, I_COUNT
+};
+enum Mode : int { M_INIT = 0, M_PROBE = 1, M_TRAJ = 2, M_PAUSED = 3, M_DONE = 4, M_ERROR = 5 };
+enum Counter : int { C_GRAD, C_LEAP, C_DIV, C_COUNT };
+constexpr int N_STATS = 6;
+
+struct NutsArgs {
+  int nchains, C, Dp, family;
+  int max_depth, num_warmup, num_samples, total_iters;
+  int adapt, var_on, skip_ss, iter_offset;
+  unsigned init_buffer, term_buffer, base_window;
+  double delta, gamma, kappa, t0;
+  uint64_t seed;
+  int S_total, Pmax;
+  const ShardDev* shards;
+  double* vec;      // nchains * V_COUNT * Dp
+  double* stk;      // nchains * max_depth * SV_COUNT * Dp
+  double* sc;       // nchains * S_COUNT
+  double* stks;     // nchains * max_depth * SS_COUNT
+  int* iv;          // nchains * I_COUNT
+  unsigned long long* cnt;  // nchains * C_COUNT
+  double* qeval;    // nchains * Dp   requested evaluation points
+  double* lp_in;    // nchains        lp at the requested points
+  double* g_in;     // nchains * Dp   grad lp at the requested points
+  double* draws;    // nshards * Pmax * S_total   (P x S per shard, chain-major columns)
+  double* stats;    // nshards * S_total * N_STATS
+  double* udraws;   // nchains * num_samples * Dp
+  int* req_step;    // nshards: last step index that issued a request for the shard
+  const int* shard_ids;  // nullptr or global shard index per local shard (RNG stream keys)
+};
+
+// RNG stream of a chain: global shard index * chains + chain.
+__host__ __device__ inline uint32_t rng_stream(const NutsArgs& A, int gid) {
+  const int s = gid / A.C;
+  return (uint32_t)((A.shard_ids ? A.shard_ids[s] : s) * A.C + gid % A.C);
+}
+
+}  // namespace stk
+
+// Error plumbing for the C-ABI layer.
+void stk_set_error(const char* fmt, ...);
+#define STK_HIP_CHECK(expr)                                                        \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) {                                                        \
+      stk_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+      return STK_E_HIP;                                                            \
+    }                                                                              \
+  } while (0)

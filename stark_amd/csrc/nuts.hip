@@ -1,0 +1,717 @@
+// Batched NUTS for gfx950: one wavefront per chain, an ITERATIVE per-chain state machine.
+//
+// Replaces Stan's hmc_nuts_diag_e_adapt, which stark runs once per Spark partition inside
+// `sm.sampling(data=data, **kwargs)` (stark/stark.py:48).  Algorithm = Stan 2.19.1
+// base_nuts::transition / build_tree (restated in oracle/stark_oracle.c, which keeps the
+// recursive form), rewritten so that one call advances a chain by exactly ONE leapfrog step:
+//
+//   consume the gradient at the point requested last step
+//     -> finish the leapfrog -> leaf bookkeeping -> merge completed sub-trees (binary
+//        counter over the leaf index; pending left sub-trees live on a per-level stack)
+//     -> top-level multinomial / U-turn / depth checks -> maybe end the transition
+//        (draw, dual averaging, Welford windows, init_stepsize probes) and start the next
+//     -> half-step p, full-step q, request the gradient at the new q.
+//
+// A chain that finishes its transition starts the next one on the very next step, so
+// chains of one wave group never idle behind each other's tree depth (the SIMD-lockstep
+// problem of recursive NUTS).  Lanes hold dimensions (64 per chunk, NCH chunks), every
+// scalar is wave-uniform (reductions broadcast lane 0's value), and every uniform value
+// is stored by all lanes, so each lane only ever re-reads its own writes.
+//
+// Two drivers share the state machine:
+//   k_nuts_step   split mode: the gradient comes from the data-sweep kernels (sweep.hip),
+//                 one launch per leapfrog for all chains of all local shards;
+//   k_nuts_fused  local models (8 schools): the gradient is computed inline and each wave
+//                 loops its own chain for up to max_steps leapfrogs in ONE launch.
+#include "common.h"
+#include <math.h>
+
+namespace stk {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return __shfl(v, 0, WAVE);   // broadcast: identical bits in every lane
+}
+
+__device__ __forceinline__ double log_sum_exp2(double a, double b) {   // stan::math::log_sum_exp
+  if (a == -INFINITY) return b;
+  if (a == INFINITY && b == INFINITY) return INFINITY;
+  if (a > b) return a + log1p(exp(b - a));
+  return b + log1p(exp(a - b));
+}
+
+// ------------------------------------------------------------------ model hooks
+// 8 schools (example/schools.stan:1-18): q = (mu, log tau, eta_1..J); returns lp, writes
+// grad lp.  Mirrors oracle orc_schools_lpgrad.
+template <int NCH>
+__device__ double schools_lpgrad(const ShardDev& sh, const double (&q)[NCH], double (&glp)[NCH], int lane, int D) {
+  const double mu = __shfl(q[0], 0, WAVE);
+  const double u = __shfl(q[0], 1, WAVE);
+  const double tau = exp(u);
+  double lp = 0.0, smu = 0.0, su = 0.0;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int e = k * WAVE + lane;
+    glp[k] = 0.0;
+    if (e >= 2 && e < D) {
+      const int j = e - 2;
+      const double eta = q[k];
+      const double theta = mu + tau * eta;
+      const double sj = sh.sigma[j];
+      const double z = (sh.y[j] - theta) / sj;
+      const double r = z / sj;
+      lp += -0.5 * eta * eta - 0.5 * z * z;
+      smu += r;
+      su += r * eta;
+      glp[k] = -eta + tau * r;
+    }
+  }
+  lp = wave_sum(lp) + u;
+  smu = wave_sum(smu);
+  su = wave_sum(su);
+  if (lane == 0) glp[0] = smu;
+  if (lane == 1) glp[0] = tau * su + 1.0;
+  return lp;
+}
+
+// Constrained output row (extract() order: params, transformed params, lp__).
+template <int NCH>
+__device__ void write_draw(const NutsArgs& A, const ShardDev& sh, int shard, int col, const double (&q)[NCH],
+                           double lp, int lane) {
+  double* out = A.draws + (size_t)shard * A.Pmax * A.S_total;
+  const int D = sh.D;
+  const size_t S = (size_t)A.S_total;
+  if (A.family == STK_SCHOOLS) {
+    const double mu = __shfl(q[0], 0, WAVE);
+    const double tau = exp(__shfl(q[0], 1, WAVE));
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int e = k * WAVE + lane;
+      if (e < D) out[(size_t)e * S + col] = (e == 1) ? tau : q[k];
+      if (e >= 2 && e < D) out[(size_t)(D + e - 2) * S + col] = mu + tau * q[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int e = k * WAVE + lane;
+      if (e < D) out[(size_t)e * S + col] = (A.family == STK_LINREG && e == D - 1) ? exp(q[k]) : q[k];
+    }
+  }
+  if (lane == 0) out[(size_t)(sh.P - 1) * S + col] = lp;
+}
+
+// ------------------------------------------------------------------ the chain
+template <int NCH>
+struct NutsChain {
+  const NutsArgs& A;
+  const int gid, lane, shard, cidx, D;
+  const uint32_t rid;   // RNG stream id (global shard * chains + chain)
+  const ShardDev& sh;
+  double* const vec;
+  double* const stk;
+  double* const stks;
+  double s[S_COUNT];
+  int iv[I_COUNT];
+  double q[NCH], p[NCH], g[NCH], im[NCH];
+
+  __device__ NutsChain(const NutsArgs& a, int gid_, int lane_)
+      : A(a), gid(gid_), lane(lane_), shard(gid_ / a.C), cidx(gid_ % a.C), D(a.shards[gid_ / a.C].D),
+        rid(rng_stream(a, gid_)),
+        sh(a.shards[gid_ / a.C]),
+        vec(a.vec + (size_t)gid_ * V_COUNT * a.Dp),
+        stk(a.stk + (size_t)gid_ * a.max_depth * SV_COUNT * a.Dp),
+        stks(a.stks + (size_t)gid_ * a.max_depth * SS_COUNT) {}
+
+  __device__ __forceinline__ bool ok(int k) const { return k * WAVE + lane < D; }
+  __device__ __forceinline__ double* vp(int v) const { return vec + (size_t)v * A.Dp; }
+  __device__ __forceinline__ double* svp(int level, int v) const {
+    return stk + ((size_t)level * SV_COUNT + v) * A.Dp;
+  }
+  __device__ void ld(const double* base, double (&r)[NCH]) const {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) r[k] = ok(k) ? base[k * WAVE + lane] : 0.0;
+  }
+  __device__ void st(double* base, const double (&r)[NCH]) const {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+      if (ok(k)) base[k * WAVE + lane] = r[k];
+  }
+
+  __device__ void load() {
+    const double* sc = A.sc + (size_t)gid * S_COUNT;
+    const int* ivp = A.iv + (size_t)gid * I_COUNT;
+#pragma unroll
+    for (int i = 0; i < S_COUNT; ++i) s[i] = sc[i];
+#pragma unroll
+    for (int i = 0; i < I_COUNT; ++i) iv[i] = ivp[i];
+    ld(vp(V_Q), q);
+    ld(vp(V_P), p);
+    ld(vp(V_G), g);
+    ld(vp(V_IM), im);
+  }
+  __device__ void save() const {
+    double* sc = A.sc + (size_t)gid * S_COUNT;
+    int* ivp = A.iv + (size_t)gid * I_COUNT;
+#pragma unroll
+    for (int i = 0; i < S_COUNT; ++i) sc[i] = s[i];
+#pragma unroll
+    for (int i = 0; i < I_COUNT; ++i) ivp[i] = iv[i];
+    st(vp(V_Q), q);
+    st(vp(V_P), p);
+    st(vp(V_G), g);
+  }
+
+  __device__ double kinetic(const double (&pp)[NCH]) const {   // diag_e_metric::tau
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+      if (ok(k)) t += pp[k] * im[k] * pp[k];
+    return 0.5 * wave_sum(t);
+  }
+  __device__ bool criterion(const double (&psm)[NCH], const double (&psp)[NCH], const double (&rho)[NCH]) const {
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+      if (ok(k)) { a += psp[k] * rho[k]; b += psm[k] * rho[k]; }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    return a > 0 && b > 0;
+  }
+  __device__ double uniform() {
+    const uint32_t it = (uint32_t)(iv[I_ITER] + A.iter_offset);
+    return uniform_at(A.seed, rid, it, (uint32_t)iv[I_UK]++, TAG_UNI);
+  }
+  __device__ void sample_momentum(uint32_t c1, uint32_t c2hi, uint32_t tag) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int e = k * WAVE + lane;
+      p[k] = ok(k) ? normal_at(A.seed, rid, c1, c2hi, (uint32_t)e, tag) / sqrt(im[k]) : 0.0;
+    }
+  }
+  __device__ void load_sample_point() {
+    ld(vp(V_QS), q);
+    ld(vp(V_GS), g);
+    s[S_V] = s[S_VS];
+  }
+
+  // Request = the new q after begin_update_p + update_q (expl_leapfrog).
+  __device__ void begin_leapfrog(double eps) {
+    s[S_LFEPS] = eps;
+    const double he = 0.5 * eps;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      p[k] -= he * g[k];
+      q[k] += eps * (im[k] * p[k]);
+    }
+  }
+  __device__ void finish_leapfrog(double lp, const double (&glp)[NCH]) {
+    const double he = 0.5 * s[S_LFEPS];
+    s[S_V] = -lp;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      g[k] = -glp[k];
+      p[k] -= he * g[k];
+    }
+  }
+
+  // ---- init_stepsize (base_hmc) as a probe sequence, one leapfrog per step
+  __device__ bool start_probe() {
+    const double e = s[S_NOMEPS];
+    if (e == 0 || e > 1e7 || isnan(e)) return false;
+    iv[I_PROBE] = 0;
+    iv[I_MODE] = M_PROBE;
+    load_sample_point();
+    sample_momentum((uint32_t)iv[I_SSCALL], 0u, TAG_SSMOM);
+    s[S_PH0] = s[S_V] + kinetic(p);
+    begin_leapfrog(e);
+    return true;
+  }
+
+  // ---- adaptation (stepsize_adaptation, windowed var_adaptation)
+  __device__ void learn_stepsize(double adapt_stat) {
+    s[S_DA_CNT] += 1.0;
+    adapt_stat = adapt_stat > 1 ? 1 : adapt_stat;
+    const double eta = 1.0 / (s[S_DA_CNT] + A.t0);
+    s[S_SBAR] = (1.0 - eta) * s[S_SBAR] + eta * (A.delta - adapt_stat);
+    const double x = s[S_MU] - s[S_SBAR] * sqrt(s[S_DA_CNT]) / A.gamma;
+    const double x_eta = pow(s[S_DA_CNT], -A.kappa);
+    s[S_XBAR] = (1.0 - x_eta) * s[S_XBAR] + x_eta * x;
+    s[S_NOMEPS] = exp(x);
+  }
+  __device__ bool learn_variance() {
+    const unsigned cnt = (unsigned)iv[I_WCNT];
+    const unsigned nw = (unsigned)A.num_warmup;
+    const bool in_window = (cnt >= A.init_buffer) && (cnt < nw - A.term_buffer) && (cnt != nw);
+    double wm[NCH], wm2[NCH];
+    ld(vp(V_WM), wm);
+    ld(vp(V_WM2), wm2);
+    if (in_window) {
+      double qs[NCH];
+      ld(vp(V_QS), qs);
+      s[S_WFN] += 1.0;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const double delta = qs[k] - wm[k];
+        wm[k] += delta / s[S_WFN];
+        wm2[k] += (qs[k] - wm[k]) * delta;
+      }
+    }
+    const bool end_window = (cnt == (unsigned)iv[I_WNEXT]) && (cnt != nw);
+    if (end_window) {
+      // compute_next_window
+      const unsigned last = nw - A.term_buffer - 1;
+      if ((unsigned)iv[I_WNEXT] != last) {
+        unsigned size = (unsigned)iv[I_WSIZE] * 2;
+        unsigned next = cnt + size;
+        if (next != last) {
+          const unsigned nb = next + 2 * size;
+          if (nb >= nw - A.term_buffer) next = last;
+        }
+        iv[I_WSIZE] = (int)size;
+        iv[I_WNEXT] = (int)next;
+      }
+      const double n = s[S_WFN];
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        double v = im[k];
+        if (n > 1) v = wm2[k] / (n - 1.0);
+        im[k] = (n / (n + 5.0)) * v + 1e-3 * (5.0 / (n + 5.0));
+        wm[k] = 0.0;
+        wm2[k] = 0.0;
+      }
+      s[S_WFN] = 0.0;
+      st(vp(V_IM), im);
+    }
+    st(vp(V_WM), wm);
+    st(vp(V_WM2), wm2);
+    iv[I_WCNT] = (int)(cnt + 1);
+    return end_window;
+  }
+
+  // ---- transitions
+  __device__ void begin_subtree() {
+    iv[I_DIR] = uniform() > 0.5 ? 1 : -1;
+    const int f = iv[I_DIR] > 0;
+    ld(vp(f ? V_QF : V_QB), q);
+    ld(vp(f ? V_PF : V_PB), p);
+    ld(vp(f ? V_GF : V_GB), g);
+    s[S_V] = f ? s[S_VF] : s[S_VB];
+    iv[I_LEAF] = 0;
+    begin_leapfrog(iv[I_DIR] * s[S_EPS]);
+  }
+
+  __device__ void start_transition() {
+    iv[I_MODE] = M_TRAJ;
+    s[S_EPS] = s[S_NOMEPS];
+    iv[I_UK] = 0;
+    load_sample_point();
+    sample_momentum((uint32_t)(iv[I_ITER] + A.iter_offset), 0u, TAG_MOM);
+    const double H0 = s[S_V] + kinetic(p);
+    s[S_H0] = H0;
+    s[S_HS] = H0;
+    st(vp(V_QF), q); st(vp(V_PF), p); st(vp(V_GF), g);
+    st(vp(V_QB), q); st(vp(V_PB), p); st(vp(V_GB), g);
+    s[S_VF] = s[S_V];
+    s[S_VB] = s[S_V];
+    double ps[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) ps[k] = im[k] * p[k];
+    st(vp(V_PSP), ps);
+    st(vp(V_PSM), ps);
+    st(vp(V_RHO), p);
+    s[S_LSW] = 0.0;
+    s[S_SUMMETRO] = 0.0;
+    iv[I_NLEAP] = 0;
+    iv[I_DEPTH] = 0;
+    iv[I_DIV] = 0;
+    begin_subtree();
+  }
+
+  // After a transition (or its adaptation probes): stop, pause or go on.  Returns true
+  // if a gradient request was issued.
+  __device__ bool continue_or_stop(int pause_at) {
+    if (iv[I_ITER] >= A.total_iters) { iv[I_MODE] = M_DONE; return false; }
+    if (iv[I_ITER] >= pause_at) { iv[I_MODE] = M_PAUSED; return false; }
+    start_transition();
+    return true;
+  }
+
+  __device__ bool end_transition(int pause_at) {
+    const double accept = s[S_SUMMETRO] / (double)iv[I_NLEAP];
+    const int it = iv[I_ITER];
+    if (it >= A.num_warmup) {
+      const int col = cidx * A.num_samples + (it - A.num_warmup);
+      double qs[NCH];
+      ld(vp(V_QS), qs);
+      write_draw<NCH>(A, sh, shard, col, qs, -s[S_VS], lane);
+      double* ud = A.udraws + ((size_t)gid * A.num_samples + (it - A.num_warmup)) * A.Dp;
+      st(ud, qs);
+      if (lane < N_STATS) {
+        double v = 0;
+        switch (lane) {
+          case 0: v = accept; break;
+          case 1: v = s[S_EPS]; break;
+          case 2: v = (double)iv[I_DEPTH]; break;
+          case 3: v = (double)iv[I_NLEAP]; break;
+          case 4: v = (double)iv[I_DIV]; break;
+          default: v = s[S_HS]; break;
+        }
+        A.stats[((size_t)shard * A.S_total + col) * N_STATS + lane] = v;
+      }
+      if (iv[I_DIV] && lane == 0) A.cnt[(size_t)gid * C_COUNT + C_DIV] += 1;
+    }
+    bool update = false;
+    if (A.adapt && it < A.num_warmup) {
+      learn_stepsize(accept);
+      if (A.var_on) update = learn_variance();
+    }
+    iv[I_ITER] = it + 1;
+    if (update) {
+      iv[I_SSREASON] = (A.adapt && it + 1 == A.num_warmup) ? 2 : 1;
+      if (start_probe()) return true;
+      finish_window_update();
+    } else if (A.adapt && it + 1 == A.num_warmup) {
+      s[S_NOMEPS] = exp(s[S_XBAR]);   // complete_adaptation
+    }
+    return continue_or_stop(pause_at);
+  }
+
+  __device__ void finish_window_update() {
+    s[S_MU] = log(10.0 * s[S_NOMEPS]);
+    s[S_DA_CNT] = 0.0;
+    s[S_SBAR] = 0.0;
+    s[S_XBAR] = 0.0;
+    if (iv[I_SSREASON] == 2) s[S_NOMEPS] = exp(s[S_XBAR]);
+  }
+
+  __device__ bool on_probe(double lp, const double (&glp)[NCH], int pause_at) {
+    finish_leapfrog(lp, glp);
+    double h = s[S_V] + kinetic(p);
+    if (isnan(h)) h = INFINITY;
+    const double dH = s[S_PH0] - h;
+    const double l08 = log(0.8);
+    bool more = true;
+    if (iv[I_PROBE] == 0) {
+      iv[I_PDIR] = dH > l08 ? 1 : -1;
+    } else if ((iv[I_PDIR] == 1 && !(dH > l08)) || (iv[I_PDIR] == -1 && !(dH < l08))) {
+      more = false;
+    } else {
+      s[S_NOMEPS] = iv[I_PDIR] == 1 ? 2 * s[S_NOMEPS] : 0.5 * s[S_NOMEPS];
+      if (s[S_NOMEPS] > 1e7 || s[S_NOMEPS] == 0) {
+        iv[I_MODE] = M_ERROR;
+        load_sample_point();
+        return false;
+      }
+    }
+    if (more) {
+      iv[I_PROBE] += 1;
+      load_sample_point();
+      sample_momentum((uint32_t)iv[I_SSCALL], (uint32_t)iv[I_PROBE] << 12, TAG_SSMOM);
+      s[S_PH0] = s[S_V] + kinetic(p);
+      begin_leapfrog(s[S_NOMEPS]);
+      return true;
+    }
+    iv[I_SSCALL] += 1;
+    load_sample_point();
+    if (iv[I_SSREASON] >= 1) finish_window_update();
+    return continue_or_stop(pause_at);
+  }
+
+  __device__ bool on_leaf(double lp, const double (&glp)[NCH], int pause_at) {
+    finish_leapfrog(lp, glp);
+    if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_LEAP] += 1;
+    const double H0 = s[S_H0];
+    double h = s[S_V] + kinetic(p);
+    if (isnan(h)) h = INFINITY;
+    if ((h - H0) > 1000.0) iv[I_DIV] = 1;
+    iv[I_NLEAP] += 1;
+    s[S_SUMMETRO] += (H0 - h > 0) ? 1.0 : exp(H0 - h);
+    // the leaf as a depth-0 sub-tree
+    double c_lsw = H0 - h;
+    double c_rho[NCH], c_psb[NCH], c_pse[NCH], c_q[NCH], c_g[NCH];
+    double c_V = s[S_V], c_H = h;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      c_rho[k] = p[k];
+      c_psb[k] = im[k] * p[k];
+      c_pse[k] = c_psb[k];
+      c_q[k] = q[k];
+      c_g[k] = g[k];
+    }
+    if (iv[I_DIV]) return end_transition(pause_at);
+    const int depth = iv[I_DEPTH];
+    const int n = iv[I_LEAF];
+    int j = 0;
+    while (j < depth && ((n >> j) & 1)) {
+      // merge pending left sub-tree (level j) with the just-completed right one
+      const double l_lsw = stks[j * SS_COUNT + SS_LSW];
+      double l_rho[NCH], l_psb[NCH];
+      ld(svp(j, SV_RHO), l_rho);
+      ld(svp(j, SV_PSB), l_psb);
+      const double lsw_sub = log_sum_exp2(l_lsw, c_lsw);
+      const double u = uniform();
+      const bool take_right = (c_lsw > lsw_sub) || (u < exp(c_lsw - lsw_sub));
+      if (!take_right) {
+        ld(svp(j, SV_Q), c_q);
+        ld(svp(j, SV_G), c_g);
+        c_V = stks[j * SS_COUNT + SS_V];
+        c_H = stks[j * SS_COUNT + SS_H];
+      }
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        c_rho[k] = l_rho[k] + c_rho[k];
+        c_psb[k] = l_psb[k];
+      }
+      c_lsw = lsw_sub;
+      if (!criterion(l_psb, c_pse, c_rho)) return end_transition(pause_at);
+      ++j;
+    }
+    if (j < depth) {
+      // push the completed sub-tree as the pending left sub-tree of level j
+      st(svp(j, SV_RHO), c_rho);
+      st(svp(j, SV_PSB), c_psb);
+      st(svp(j, SV_Q), c_q);
+      st(svp(j, SV_G), c_g);
+      stks[j * SS_COUNT + SS_LSW] = c_lsw;
+      stks[j * SS_COUNT + SS_V] = c_V;
+      stks[j * SS_COUNT + SS_H] = c_H;
+      iv[I_LEAF] = n + 1;
+      begin_leapfrog(iv[I_DIR] * s[S_EPS]);
+      return true;
+    }
+    // the top-level sub-tree of this depth is complete and valid
+    const int fwd = iv[I_DIR] > 0;
+    st(vp(fwd ? V_QF : V_QB), q);
+    st(vp(fwd ? V_PF : V_PB), p);
+    st(vp(fwd ? V_GF : V_GB), g);
+    s[fwd ? S_VF : S_VB] = s[S_V];
+    iv[I_DEPTH] = depth + 1;
+    const double u = uniform();
+    if (c_lsw > s[S_LSW] || u < exp(c_lsw - s[S_LSW])) {
+      st(vp(V_QS), c_q);
+      st(vp(V_GS), c_g);
+      s[S_VS] = c_V;
+      s[S_HS] = c_H;
+    }
+    s[S_LSW] = log_sum_exp2(s[S_LSW], c_lsw);
+    double rho[NCH], psp[NCH], psm[NCH];
+    ld(vp(V_RHO), rho);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) rho[k] = rho[k] + c_rho[k];
+    st(vp(V_RHO), rho);
+    if (fwd) {
+      st(vp(V_PSP), c_pse);
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) psp[k] = c_pse[k];
+      ld(vp(V_PSM), psm);
+    } else {
+      st(vp(V_PSM), c_pse);
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) psm[k] = c_pse[k];
+      ld(vp(V_PSP), psp);
+    }
+    if (!criterion(psm, psp, rho) || iv[I_DEPTH] >= A.max_depth) return end_transition(pause_at);
+    begin_subtree();
+    return true;
+  }
+
+  // Consume the evaluation requested last step.  Returns true if a new request (at q) was issued.
+  __device__ bool consume(double lp, const double (&glp)[NCH], int pause_at) {
+    switch (iv[I_MODE]) {
+      case M_INIT: {
+        s[S_V] = -lp;
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) g[k] = -glp[k];
+        st(vp(V_QS), q);
+        st(vp(V_GS), g);
+        s[S_VS] = s[S_V];
+        iv[I_SSREASON] = 0;
+        if (!A.skip_ss && start_probe()) return true;
+        return continue_or_stop(pause_at);
+      }
+      case M_PROBE: return on_probe(lp, glp, pause_at);
+      case M_TRAJ: return on_leaf(lp, glp, pause_at);
+      default: return false;
+    }
+  }
+
+  __device__ bool resume(int pause_at) {   // PAUSED -> next transition
+    if (iv[I_MODE] != M_PAUSED) return false;
+    return continue_or_stop(pause_at);
+  }
+};
+
+// ------------------------------------------------------------------ kernels
+__global__ __launch_bounds__(64) void k_nuts_init(NutsArgs A, const double* init, const double* inv_metric,
+                                                  double stepsize, double init_radius) {
+  const int gid = blockIdx.x, lane = threadIdx.x;
+  const ShardDev& sh = A.shards[gid / A.C];
+  const int D = sh.D;
+  double* vec = A.vec + (size_t)gid * V_COUNT * A.Dp;
+  for (int v = 0; v < V_COUNT; ++v)
+    for (int e = lane; e < A.Dp; e += WAVE) vec[(size_t)v * A.Dp + e] = 0.0;
+  for (int e = lane; e < A.Dp; e += WAVE) {
+    double q0 = 0.0, imv = 1.0;
+    if (e < D) {
+      q0 = init ? init[(size_t)gid * D + e]
+                : -init_radius + 2.0 * init_radius * uniform_at(A.seed, rng_stream(A, gid), 0u, (uint32_t)e, TAG_INIT);
+      if (inv_metric) imv = inv_metric[e];
+    }
+    vec[(size_t)V_Q * A.Dp + e] = q0;
+    vec[(size_t)V_QS * A.Dp + e] = q0;
+    vec[(size_t)V_IM * A.Dp + e] = imv;
+    A.qeval[(size_t)gid * A.Dp + e] = q0;
+  }
+  double* sc = A.sc + (size_t)gid * S_COUNT;
+  for (int i = lane; i < S_COUNT; i += WAVE) sc[i] = 0.0;
+  int* ivp = A.iv + (size_t)gid * I_COUNT;
+  for (int i = lane; i < I_COUNT; i += WAVE) ivp[i] = 0;
+  for (int i = lane; i < C_COUNT; i += WAVE) A.cnt[(size_t)gid * C_COUNT + i] = 0;
+  __syncthreads();
+  if (lane == 0) {
+    sc[S_NOMEPS] = stepsize;
+    sc[S_EPS] = stepsize;
+    sc[S_MU] = log(10.0 * stepsize);
+    ivp[I_MODE] = M_INIT;
+    ivp[I_WCNT] = 0;
+    ivp[I_WSIZE] = (int)A.base_window;
+    ivp[I_WNEXT] = (int)(A.init_buffer + A.base_window - 1);
+    A.cnt[(size_t)gid * C_COUNT + C_GRAD] = 1;   // the evaluation at q0
+    A.req_step[gid / A.C] = -1;
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(64) void k_nuts_step(NutsArgs A, int step_id, int pause_at) {
+  const int gid = blockIdx.x, lane = threadIdx.x;
+  NutsChain<NCH> ch(A, gid, lane);
+  ch.load();
+  const int mode = ch.iv[I_MODE];
+  if (mode == M_DONE || mode == M_ERROR) return;
+  bool req;
+  if (mode == M_PAUSED) {
+    if (ch.iv[I_ITER] >= pause_at) return;
+    req = ch.resume(pause_at);
+  } else {
+    double glp[NCH];
+    ch.ld(A.g_in + (size_t)gid * A.Dp, glp);
+    req = ch.consume(A.lp_in[gid], glp, pause_at);
+  }
+  ch.save();
+  if (req) {
+    ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);
+    A.req_step[ch.shard] = step_id;
+    if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += 1;
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(64) void k_nuts_fused_schools(NutsArgs A, int pause_at, int max_steps) {
+  const int gid = blockIdx.x, lane = threadIdx.x;
+  NutsChain<NCH> ch(A, gid, lane);
+  ch.load();
+  const int mode = ch.iv[I_MODE];
+  if (mode == M_DONE || mode == M_ERROR) return;
+  bool req;
+  if (mode == M_PAUSED) {
+    if (ch.iv[I_ITER] >= pause_at) return;
+    req = ch.resume(pause_at);
+    if (req && lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += 1;
+  } else {
+    ch.ld(A.qeval + (size_t)gid * A.Dp, ch.q);   // the pending request
+    req = true;
+  }
+  int steps = 0;
+  unsigned long long ngrad = 0;
+  while (req && steps < max_steps) {
+    double glp[NCH];
+    const double lp = schools_lpgrad<NCH>(ch.sh, ch.q, glp, lane, ch.D);
+    ++steps;
+    req = ch.consume(lp, glp, pause_at);
+    if (req) ++ngrad;
+  }
+  ch.save();
+  if (req) ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);
+  if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += ngrad;
+}
+
+// lp / gradient of the 8-schools density at C points of one shard (parity hook).
+template <int NCH>
+__global__ __launch_bounds__(64) void k_schools_lpgrad(const ShardDev* shards, int shard, const double* q, int Dp,
+                                                       double* lp, double* g) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const ShardDev& sh = shards[shard];
+  double qq[NCH], gl[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int e = k * WAVE + lane;
+    qq[k] = e < sh.D ? q[(size_t)c * Dp + e] : 0.0;
+  }
+  const double v = schools_lpgrad<NCH>(sh, qq, gl, lane, sh.D);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int e = k * WAVE + lane;
+    if (e < sh.D) g[(size_t)c * Dp + e] = gl[k];
+  }
+  if (lane == 0) lp[c] = v;
+}
+
+}  // namespace stk
+
+// ------------------------------------------------------------------ launchers
+using namespace stk;
+
+template <int NCH>
+static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hipStream_t st) {
+  hipLaunchKernelGGL(k_nuts_step<NCH>, dim3(A.nchains), dim3(64), 0, st, A, step_id, pause_at);
+  return hipGetLastError();
+}
+template <int NCH>
+static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
+  hipLaunchKernelGGL(k_nuts_fused_schools<NCH>, dim3(A.nchains), dim3(64), 0, st, A, pause_at, max_steps);
+  return hipGetLastError();
+}
+
+int stk_nch_for(int Dmax) {
+  if (Dmax <= 64) return 1;
+  if (Dmax <= 128) return 2;
+  if (Dmax <= 256) return 4;
+  if (Dmax <= 1024) return 16;
+  return -1;
+}
+
+hipError_t stk_launch_nuts_init(const NutsArgs& A, const double* init, const double* inv_metric, double stepsize,
+                                double init_radius, hipStream_t st) {
+  hipLaunchKernelGGL(k_nuts_init, dim3(A.nchains), dim3(64), 0, st, A, init, inv_metric, stepsize, init_radius);
+  return hipGetLastError();
+}
+
+hipError_t stk_launch_nuts_step(const NutsArgs& A, int nch, int step_id, int pause_at, hipStream_t st) {
+  switch (nch) {
+    case 1: return launch_step_t<1>(A, step_id, pause_at, st);
+    case 2: return launch_step_t<2>(A, step_id, pause_at, st);
+    case 4: return launch_step_t<4>(A, step_id, pause_at, st);
+    case 16: return launch_step_t<16>(A, step_id, pause_at, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t stk_launch_nuts_fused(const NutsArgs& A, int nch, int pause_at, int max_steps, hipStream_t st) {
+  switch (nch) {
+    case 1: return launch_fused_t<1>(A, pause_at, max_steps, st);
+    case 2: return launch_fused_t<2>(A, pause_at, max_steps, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t stk_launch_schools_lpgrad(const ShardDev* shards, int shard, int nch, const double* q, int C, int Dp,
+                                     double* lp, double* g, hipStream_t st) {
+  if (nch == 1)
+    hipLaunchKernelGGL(k_schools_lpgrad<1>, dim3(C), dim3(64), 0, st, shards, shard, q, Dp, lp, g);
+  else if (nch == 2)
+    hipLaunchKernelGGL(k_schools_lpgrad<2>, dim3(C), dim3(64), 0, st, shards, shard, q, Dp, lp, g);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}

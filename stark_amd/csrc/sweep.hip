@@ -1,0 +1,360 @@
+// Regression log-density + gradient sweeps for gfx950 (the HBM-bound hot kernel).
+//
+// Replaces the gradient Stan's reverse-mode autodiff computes for every leapfrog inside
+// `sm.sampling` (stark/stark.py:48) for the build's regression programs
+// (stark_amd/models/logistic.stan, linear.stan; oracle: orc_logreg_lpgrad / orc_linreg_lpgrad).
+//
+// One pass over a shard's X serves all C chains of the shard: a 256-thread workgroup
+// streams a chunk of rows in tiles of T rows (T*d*8 <= 64 KB), staged through LDS with a
+// register prefetch of the next tile (global_load_dwordx4 in flight while the current tile
+// is computed), and for each tile computes
+//   forward   eta[r][c] = alpha_c + x_r . beta_c       (S = 256/T lanes per row, xor-reduce)
+//   residual  d eta[r][c] and the lp terms            (Stan's +-20 cutoff for bernoulli_logit)
+//   backward  g[j][c]  += sum_r x_r[j] * d eta[r][c]  (lanes over columns, rows split RG ways)
+// so X crosses HBM exactly once per leapfrog: algorithmic bytes per sweep = n*(8d + 4)
+// (logreg, int32 y) or n*(8d + 8) (linreg).  Each shard is cut into G chunks that depend
+// only on (n, d); per-chunk partial sums are reduced in chunk order by k_sweep_reduce, so
+// results are bitwise independent of how many shards share a GPU.
+#include "common.h"
+#include <math.h>
+#include <type_traits>
+
+namespace stk {
+
+struct SweepArgs {
+  const ShardDev* shards;
+  const double* q;        // [nshards*C][Dp] evaluation points
+  double* partial;        // [nshards][G][C][PW]
+  const int* req_step;    // nullptr: always run
+  int step_id;
+  int C, Dp, G, LD, PW;
+  int shard0;             // first shard of this launch
+  int Gs;                 // partial-buffer stride in chunks per shard (>= G)
+  int* ran;               // optional: ran[step_id & 63] = 1 when any shard swept
+};
+
+template <int FAM, int C, int T, int JPT, int VEC>
+__global__ __launch_bounds__(256) void k_sweep(SweepArgs A) {
+  constexpr int NT = 256;
+  constexpr int S = NT / T;        // lanes per row in the forward pass
+  constexpr int NVMAX = (8192 / VEC + NT - 1) / NT;
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);   // shards swept
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d, LD = A.LD, tid = threadIdx.x;
+  const int64_t r0 = sh.n * chunk / A.G, r1 = sh.n * (chunk + 1) / A.G;
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* Xs = lds;                       // T * LD
+  double* Bs = Xs + T * LD;               // C * LD   (beta_c)
+  double* Rs = Bs + C * LD;               // T * C    (d eta)
+  double* Al = Rs + T * C;                // C        (alpha_c) + C (inv sigma)
+
+  for (int i = tid; i < C * d; i += NT) {
+    const int c = i / d, j = i % d;
+    Bs[c * LD + j] = A.q[(size_t)(shard * C + c) * A.Dp + 1 + j];
+  }
+  if (tid < C) {
+    const double* qc = A.q + (size_t)(shard * C + tid) * A.Dp;
+    Al[tid] = qc[0];
+    Al[C + tid] = (FAM == STK_LINREG) ? exp(-qc[d + 1]) : 0.0;
+  }
+
+  // per-thread accumulators
+  double gacc[JPT][C];
+  double lpa[C], ga[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    lpa[c] = 0.0;
+    ga[c] = 0.0;
+#pragma unroll
+    for (int m = 0; m < JPT; ++m) gacc[m][c] = 0.0;
+  }
+  const int JW = d <= 64 ? 64 : (d <= 128 ? 128 : 256);
+  const int RG = NT / JW;
+  const int jl = tid % JW, rg = tid / JW;
+  const int fr = tid / S, fs = tid % S;   // forward mapping
+
+  // tile staging: VEC doubles per load, element e = VEC*(tid + NT*v) of the tile
+  using vec_t = typename std::conditional<VEC == 2, double2, double>::type;
+  vec_t buf[NVMAX];
+  const int64_t ntiles = (r1 - r0 + T - 1) / T;
+  auto prefetch = [&](int64_t t) {
+    const int64_t row_start = r0 + t * T;
+    const int64_t rows = (r1 - row_start) < T ? (r1 - row_start) : T;
+    const int64_t nel = rows * d;
+    const vec_t* src = reinterpret_cast<const vec_t*>(sh.x + row_start * d);
+#pragma unroll
+    for (int v = 0; v < NVMAX; ++v) {
+      const int64_t e = (int64_t)VEC * (tid + NT * v);
+      if (e < nel) buf[v] = src[tid + NT * v];
+    }
+  };
+  auto stage = [&](int64_t t) {
+    const int64_t row_start = r0 + t * T;
+    const int64_t rows = (r1 - row_start) < T ? (r1 - row_start) : T;
+    const int nel = (int)(rows * d);
+    int e = VEC * tid;
+    int row = e / d, col = e % d;
+    const int step = VEC * NT, dq = step / d, dr = step % d;
+#pragma unroll
+    for (int v = 0; v < NVMAX; ++v) {
+      if (e < nel) {
+        if constexpr (VEC == 2) {
+          *reinterpret_cast<double2*>(&Xs[row * LD + col]) = buf[v];
+        } else {
+          Xs[row * LD + col] = buf[v];
+        }
+      }
+      e += step;
+      row += dq;
+      col += dr;
+      if (col >= d) { col -= d; ++row; }
+    }
+  };
+
+  if (ntiles > 0) prefetch(0);
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int64_t row_start = r0 + t * T;
+    const int rows = (int)((r1 - row_start) < T ? (r1 - row_start) : T);
+    stage(t);
+    __syncthreads();
+    if (t + 1 < ntiles) prefetch(t + 1);
+
+    // ---- forward + residual
+    {
+      double acc[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] = 0.0;
+      if (fr < rows) {
+        const double* xr = Xs + fr * LD;
+        for (int j = fs; j < d; j += S) {
+          const double x = xr[j];
+#pragma unroll
+          for (int c = 0; c < C; ++c) acc[c] += x * Bs[c * LD + j];
+        }
+      }
+#pragma unroll
+      for (int o = S / 2; o > 0; o >>= 1)
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] += __shfl_xor(acc[c], o, 64);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        if ((c % S) != fs) continue;
+        double de = 0.0;
+        if (fr < rows) {
+          const int64_t row = row_start + fr;
+          const double eta = Al[c] + acc[c];
+          if constexpr (FAM == STK_LOGREG) {
+            const double sgn = 2.0 * sh.yi[row] - 1.0;
+            const double nt = sgn * eta;
+            const double e = exp(-nt);
+            if (nt > 20.0) { lpa[c] -= e; de = sgn * e; }
+            else if (nt < -20.0) { lpa[c] += nt; de = sgn; }
+            else { lpa[c] -= log1p(e); de = sgn * e / (e + 1.0); }
+          } else {
+            const double is = Al[C + c];
+            const double z = (sh.y[row] - eta) * is;
+            lpa[c] += z * z;          // linreg: sum of squares, finished in the reduce
+            de = z * is;
+          }
+          ga[c] += de;
+        }
+        Rs[fr * C + c] = de;
+      }
+    }
+    __syncthreads();
+
+    // ---- backward: g[j][c] += x[r][j] * d eta[r][c]
+    for (int r = rg; r < rows; r += RG) {
+      const double* xr = Xs + r * LD;
+      double rr[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) rr[c] = Rs[r * C + c];
+#pragma unroll
+      for (int m = 0; m < JPT; ++m) {
+        const int j = jl + m * JW;
+        if (j < d) {
+          const double x = xr[j];
+#pragma unroll
+          for (int c = 0; c < C; ++c) gacc[m][c] += x * rr[c];
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- block reduction in a fixed order, then one partial row per chain
+  double* red = lds;   // reuse: RG * C * JW*JPT  and  NT * 2C
+  double* out = A.partial + ((size_t)shard * A.Gs + chunk) * C * A.PW;
+#pragma unroll
+  for (int m = 0; m < JPT; ++m)
+#pragma unroll
+    for (int c = 0; c < C; ++c) red[((size_t)rg * C + c) * (JW * JPT) + m * JW + jl] = gacc[m][c];
+  __syncthreads();
+  for (int i = tid; i < C * d; i += NT) {
+    const int c = i / d, j = i % d;
+    double v = 0.0;
+    for (int g = 0; g < RG; ++g) v += red[((size_t)g * C + c) * (JW * JPT) + j];
+    out[(size_t)c * A.PW + 1 + j] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    red[(size_t)c * NT + tid] = lpa[c];
+    red[(size_t)(C + c) * NT + tid] = ga[c];
+  }
+  __syncthreads();
+  if (tid < 2 * C) {
+    const int c = tid % C;
+    const bool is_lp = tid < C;
+    const double* src = red + (size_t)(is_lp ? c : C + c) * NT;
+    double v = 0.0;
+    for (int i = 0; i < NT; ++i) v += src[i];
+    out[(size_t)c * A.PW + (is_lp ? d + 1 : 0)] = v;
+  }
+}
+
+// Sum chunk partials in chunk order and finish the family's lp / gradient.
+// grid (nshards*C, ceil(PW/64)), 256 threads: 4 waves split the chunks, fixed combine order.
+template <int FAM>
+__global__ __launch_bounds__(256) void k_sweep_reduce(SweepArgs A, double* lp_out, double* g_out, int C) {
+  const int gidl = blockIdx.x;              // local chain index in this launch
+  const int shard = A.shard0 + gidl / C, c = gidl % C;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d;
+  const int o = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
+  __shared__ double part[4][64];
+  double v = 0.0;
+  if (o < A.PW) {
+    const int per = (A.G + 3) / 4;
+    const int k0 = w * per, k1 = min(A.G, k0 + per);
+    const double* src = A.partial + ((size_t)shard * A.Gs * C + c) * A.PW + o;
+    const size_t stride = (size_t)C * A.PW;
+    int k = k0;
+    for (; k + 4 <= k1; k += 4) {
+      const double a0 = src[(size_t)k * stride], a1 = src[(size_t)(k + 1) * stride];
+      const double a2 = src[(size_t)(k + 2) * stride], a3 = src[(size_t)(k + 3) * stride];
+      v += a0; v += a1; v += a2; v += a3;
+    }
+    for (; k < k1; ++k) v += src[(size_t)k * stride];
+  }
+  part[w][threadIdx.x & 63] = v;
+  __syncthreads();
+  if (w != 0 || o >= A.PW) return;
+  const double t = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+  const size_t gid = (size_t)shard * C + c;
+  double* g = g_out + gid * A.Dp;
+  if (FAM == STK_LOGREG) {
+    if (o == d + 1) lp_out[gid] = t;
+    else g[o] = t;
+  } else {
+    const double u = A.q[gid * A.Dp + d + 1];
+    const double N = (double)sh.n;
+    if (o == d + 1) {
+      g[d + 1] = -N + t + 1.0;
+      lp_out[gid] = -0.5 * t - N * u + u;
+    } else {
+      g[o] = t;
+    }
+  }
+}
+
+}  // namespace stk
+
+using namespace stk;
+
+// Host-side geometry: depends only on (n, d) so reductions are identical on 1 or N GPUs.
+void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_bytes, int C) {
+  int t = 64;
+  while (t > 8 && (int64_t)t * d > 8192) t >>= 1;
+  const int m = (256 / t) % 32;   // LD = m (mod 32): conflict-free ds_read_b64 in the forward pass
+  int ld = d;
+  while ((ld % 32) != m) ++ld;
+  int64_t g = (n + (int64_t)8 * t - 1) / ((int64_t)8 * t);
+  if (g > 512) g = 512;
+  if (g < 1) g = 1;
+  *T = t;
+  *LD = ld;
+  *G = (int)g;
+  const int JW = d <= 64 ? 64 : (d <= 128 ? 128 : 256);
+  const int JPT = (d + JW - 1) / JW;
+  const size_t main = (size_t)(t * ld + C * ld + t * C + 2 * C) * sizeof(double);
+  const size_t red1 = (size_t)(256 / JW) * C * JW * JPT * sizeof(double);
+  const size_t red2 = (size_t)2 * C * 256 * sizeof(double);
+  size_t b = main;
+  if (red1 > b) b = red1;
+  if (red2 > b) b = red2;
+  *lds_bytes = b;
+}
+
+template <int FAM, int C, int T, int JPT, int VEC>
+static hipError_t launch_sweep_t(const SweepArgs& A, int nblocks, size_t lds, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)k_sweep<FAM, C, T, JPT, VEC>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_sweep<FAM, C, T, JPT, VEC>), dim3(nblocks), dim3(256), lds, st, A);
+  return hipGetLastError();
+}
+
+template <int FAM, int C, int T, int JPT>
+static hipError_t pick_vec(const SweepArgs& A, int d, int nblocks, size_t lds, hipStream_t st) {
+  if (d % 2 == 0) return launch_sweep_t<FAM, C, T, JPT, 2>(A, nblocks, lds, st);
+  return launch_sweep_t<FAM, C, T, JPT, 1>(A, nblocks, lds, st);
+}
+
+template <int FAM, int C>
+static hipError_t pick_tile(const SweepArgs& A, int d, int T, int nblocks, size_t lds, hipStream_t st) {
+  switch (T) {
+    case 64: return pick_vec<FAM, C, 64, 1>(A, d, nblocks, lds, st);
+    case 32: return pick_vec<FAM, C, 32, 1>(A, d, nblocks, lds, st);
+    case 16: return pick_vec<FAM, C, 16, 2>(A, d, nblocks, lds, st);
+    case 8: return pick_vec<FAM, C, 8, 4>(A, d, nblocks, lds, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int FAM>
+static hipError_t pick_c(const SweepArgs& A, int d, int T, int nblocks, size_t lds, hipStream_t st) {
+  switch (A.C) {
+    case 1: return pick_tile<FAM, 1>(A, d, T, nblocks, lds, st);
+    case 2: return pick_tile<FAM, 2>(A, d, T, nblocks, lds, st);
+    case 4: return pick_tile<FAM, 4>(A, d, T, nblocks, lds, st);
+    case 8: return pick_tile<FAM, 8>(A, d, T, nblocks, lds, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+bool stk_sweep_supported(int C, int d) {
+  if (!(C == 1 || C == 2 || C == 4 || C == 8)) return false;
+  return d >= 1 && d <= 1024;
+}
+
+// Launch the sweep over `nsh` shards starting at shard0 (all with the same n, d geometry).
+hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, int nsh, int d, int T, int LD,
+                            int G, int Gs, size_t lds, const double* q, int C, int Dp, double* partial,
+                            const int* req_step, int step_id, int* ran, hipStream_t st) {
+  SweepArgs A{shards_dev, q, partial, req_step, step_id, C, Dp, G, LD, d + 2, shard0, Gs, ran};
+  const int nblocks = nsh * G;
+  if (family == STK_LOGREG) return pick_c<STK_LOGREG>(A, d, T, nblocks, lds, st);
+  if (family == STK_LINREG) return pick_c<STK_LINREG>(A, d, T, nblocks, lds, st);
+  return hipErrorInvalidValue;
+}
+
+hipError_t stk_launch_sweep_reduce(int family, const ShardDev* shards_dev, int shard0, int nsh, int d, int G, int Gs,
+                                   const double* q, int C, int Dp, double* partial, const int* req_step,
+                                   int step_id, double* lp_out, double* g_out, hipStream_t st) {
+  SweepArgs A{shards_dev, q, partial, req_step, step_id, C, Dp, G, 0, d + 2, shard0, Gs, nullptr};
+  dim3 grid(nsh * C, (d + 2 + 63) / 64);
+  if (family == STK_LOGREG)
+    hipLaunchKernelGGL(k_sweep_reduce<STK_LOGREG>, grid, dim3(256), 0, st, A, lp_out, g_out, C);
+  else
+    hipLaunchKernelGGL(k_sweep_reduce<STK_LINREG>, grid, dim3(256), 0, st, A, lp_out, g_out, C);
+  return hipGetLastError();
+}

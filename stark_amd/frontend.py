@@ -1,0 +1,130 @@
+"""Stan-program front end for ``Stark.setStanModel`` (stark/stark.py:37-39).
+
+The reference compiles any Stan program with pystan (``StanModel(**kwargs)``).  This build
+has no Stan compiler: it recognises the program as one of the fixed model families whose
+log density and gradient are hand-written gfx950 kernels, and raises
+``NotImplementedError`` for anything else.  Recognition works on a normalised token
+stream (comments and whitespace removed, old ``real y[J]`` and new ``array[J] real y``
+declarations both accepted), so formatting does not matter; an explicit ``family=``
+keyword overrides it.
+"""
+from __future__ import annotations
+
+import re
+
+import numpy as np
+
+
+def _strip(code: str) -> str:
+    code = re.sub(r"/\*.*?\*/", " ", code, flags=re.S)
+    code = re.sub(r"//[^\n]*", " ", code)
+    code = re.sub(r"#[^\n]*", " ", code)
+    code = re.sub(r"\s+", " ", code)
+    code = re.sub(r"\s*([{}()\[\];,<>=~*+\-:/])\s*", r"\1", code)
+    return code.strip()
+
+
+def _blocks(code: str) -> dict:
+    out = {}
+    i = 0
+    while i < len(code):
+        m = re.compile(r"(functions|transformed data|data|transformed parameters|parameters|model|generated quantities)\{").match(code, i)
+        if not m:
+            i += 1
+            continue
+        depth, j = 1, m.end()
+        while j < len(code) and depth:
+            depth += {"{": 1, "}": -1}.get(code[j], 0)
+            j += 1
+        out[m.group(1)] = code[m.end():j - 1]
+        i = j
+    return out
+
+
+def _decl(block: str, pattern: str) -> bool:
+    return re.search(pattern, block) is not None
+
+
+def _stmts(block: str) -> list:
+    return [s for s in block.split(";") if s]
+
+
+def recognise(model_code: str) -> str:
+    """Return 'schools', 'linear' or 'logistic' for a supported Stan program."""
+    code = _strip(model_code)
+    b = _blocks(code)
+    params = b.get("parameters", "")
+    model = b.get("model", "")
+    tp = b.get("transformed parameters", "")
+    stm = sorted(_stmts(model))
+    # 8 schools, non-centred (example/schools.stan:1-18)
+    if (_decl(params, r"(^|;)real mu(;|$)") and _decl(params, r"real<lower=0>tau") and
+            _decl(params, r"(real eta\[J\]|vector\[J\]eta|array\[J\]real eta)")):
+        theta_ok = (re.search(r"theta\[j\]=mu\+tau\*eta\[j\]", tp) or re.search(r"theta=mu\+tau\*eta", tp))
+        want = sorted(["eta~normal(0,1)", "y~normal(theta,sigma)"])
+        want2 = sorted(["eta~std_normal()", "y~normal(theta,sigma)"])
+        if theta_ok and stm in (want, want2):
+            return "schools"
+    if _decl(params, r"(^|;)real alpha(;|$)") and _decl(params, r"vector\[K\]beta"):
+        if stm in (["y~bernoulli_logit(alpha+x*beta)"], ["y~bernoulli_logit(x*beta+alpha)"]):
+            if not _decl(params, r"sigma"):
+                return "logistic"
+        if stm in (["y~normal(alpha+x*beta,sigma)"], ["y~normal(x*beta+alpha,sigma)"]):
+            if _decl(params, r"real<lower=0>sigma"):
+                return "linear"
+    raise NotImplementedError(
+        "stark_amd runs a fixed set of model families on the GPU (8 schools, Bayesian linear and logistic "
+        "regression with flat priors; see stark_amd/models/*.stan).  This Stan program is not one of them; "
+        "pass family='schools'|'linear'|'logistic' if it is an equivalent program.")
+
+
+def load_program(file=None, model_code=None, family=None, **_ignored):
+    """Mirror of pystan.StanModel(file=..., model_code=...) argument handling."""
+    if family is not None:
+        if family not in ("schools", "linear", "logistic"):
+            raise ValueError(f"unknown family {family!r}")
+        return family
+    if model_code is None:
+        if file is None:
+            raise ValueError("Either file or model_code must be given (pystan.StanModel)")
+        with open(file) as f:
+            model_code = f.read()
+    return recognise(model_code)
+
+
+def pack_data(family: str, data: dict) -> dict:
+    """Validate a Stan data dict (the prepare_data_callback output, example/stark_ex.py:8-11)
+    and turn it into a shard for stk_model_create."""
+    if family == "schools":
+        J = int(data["J"])
+        y = np.asarray(data["y"], np.float64).reshape(-1)
+        s = np.asarray(data["sigma"], np.float64).reshape(-1)
+        if y.shape[0] != J or s.shape[0] != J:
+            raise ValueError(f"schools data: J = {J} but len(y) = {y.shape[0]}, len(sigma) = {s.shape[0]}")
+        if np.any(s <= 0):
+            raise ValueError("schools data: sigma must be positive (real<lower=0> sigma[J])")
+        return {"y": y, "sigma": s}
+    N, K = int(data["N"]), int(data["K"])
+    x = np.asarray(data["x"], np.float64).reshape(N, K)
+    if family == "logistic":
+        y = np.asarray(data["y"]).reshape(-1)
+        if y.shape[0] != N:
+            raise ValueError("y must have N entries")
+        return {"x": x, "y": y.astype(np.int32)}
+    y = np.asarray(data["y"], np.float64).reshape(-1)
+    if y.shape[0] != N:
+        raise ValueError("y must have N entries")
+    return {"x": x, "y": y}
+
+
+def column_names(family: str, data: dict) -> list:
+    """extract() key order flattened to rows of the P x S draw matrix (stark/stark.py:49-56)."""
+    if family == "schools":
+        J = int(data["J"])
+        return (["mu", "tau"] + [f"eta[{j}]" for j in range(1, J + 1)] + [f"theta[{j}]" for j in range(1, J + 1)]
+                + ["lp__"])
+    K = int(data["K"])
+    cols = ["alpha"] + [f"beta[{k}]" for k in range(1, K + 1)]
+    if family == "linear":
+        cols.append("sigma")
+    return cols + ["lp__"]

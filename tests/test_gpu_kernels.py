@@ -1,0 +1,140 @@
+"""GPU parity: densities, synthetic generator and combine through libstark_hip.so vs the
+CPU oracle and the reference-generated fixtures."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RTOL_LP = 1e-10   # north_star: log-density and gradient within 1e-10 relative (fp64)
+
+
+def _rel(a, b):
+    return np.abs(a - b) / np.maximum(np.abs(b), 1.0)
+
+
+# ---------------------------------------------------------------- log density + gradient
+def test_schools_lpgrad(ctx, orc):
+    from stark_amd import engine
+    rng = np.random.default_rng(1)
+    shards = [{"y": orc.SCHOOLS_Y[:4], "sigma": orc.SCHOOLS_SIGMA[:4]},
+              {"y": orc.SCHOOLS_Y, "sigma": orc.SCHOOLS_SIGMA},
+              {"y": rng.normal(0, 10, 70), "sigma": rng.uniform(5, 20, 70)}]   # J=70: two lane chunks
+    m = engine.Model(ctx, "schools", shards)
+    for s, sh in enumerate(shards):
+        om = orc.Model(orc.FAM_SCHOOLS, y=sh["y"], sigma=sh["sigma"])
+        q = rng.normal(0, 1, (5, om.D))
+        lp, g = m.log_density_grad(s, q)
+        for c in range(5):
+            olp, og = om.lpgrad(q[c])
+            assert _rel(lp[c], olp) < RTOL_LP
+            assert np.all(_rel(g[c], og) < RTOL_LP)
+
+
+@pytest.mark.parametrize("n,d", [(1, 1), (7, 3), (1000, 100), (4097, 50), (333, 129), (257, 300), (100, 700),
+                                 (5000, 2), (64, 65)])
+@pytest.mark.parametrize("family", ["logistic", "linear"])
+def test_regression_lpgrad(ctx, orc, family, n, d):
+    from stark_amd import engine
+    rng = np.random.default_rng(n * 1000 + d)
+    X = rng.uniform(-1.7, 1.7, (n, d))
+    beta = rng.normal(0, 1 / np.sqrt(d), d)
+    if family == "logistic":
+        eta = X @ beta
+        eta[: max(1, n // 50)] *= 80.0     # exercise the +-20 cutoff branches
+        y = (rng.uniform(size=n) < 1 / (1 + np.exp(-eta))).astype(np.int32)
+        om = orc.Model(orc.FAM_LOGREG, X=X, y=y)
+    else:
+        y = 0.3 + X @ beta + rng.normal(size=n)
+        om = orc.Model(orc.FAM_LINREG, X=X, y=y)
+    m = engine.Model(ctx, family, [{"x": X[: max(1, n // 3)], "y": y[: max(1, n // 3)]}, {"x": X, "y": y}])
+    C = 5
+    q = rng.normal(0, 0.2, (C, om.D))
+    if family == "logistic":
+        q[0, 1:] = beta * 40     # large |eta| rows
+    lp, g = m.log_density_grad(1, q)
+    for c in range(C):
+        olp, og = om.lpgrad(q[c])
+        assert _rel(lp[c], olp) < RTOL_LP, (c, lp[c], olp)
+        scale = np.abs(og).max() + 1.0
+        assert np.all(np.abs(g[c] - og) <= RTOL_LP * np.maximum(np.abs(og), scale * 1e-3)), (c, np.abs(g[c] - og).max())
+
+
+# ---------------------------------------------------------------- synthetic generator
+@pytest.mark.parametrize("d", [1, 7, 100])
+def test_synthetic_generator_matches_oracle(ctx, orc, d):
+    from stark_amd import engine
+    seed, rows, nsh = 99, 3001, 3
+    m = engine.Model.synthetic(ctx, "logistic", nsh, rows, d, data_seed=seed, row_offset=17)
+    beta = engine.Model.gen_beta(seed, d)
+    np.testing.assert_array_equal(beta, orc.gen_beta(seed, d))
+    for s in range(nsh):
+        got = m.copy_data(s)
+        X = orc.gen_x(seed, 17 + s * rows, rows, d)
+        np.testing.assert_array_equal(got["x"], X)     # bit-exact
+        y, margin = orc.gen_y_logistic(seed, 17 + s * rows, X, 0.0, beta)
+        diff = got["y"] != y
+        assert np.all(margin[diff] < 1e-12)             # flips only where u ~ p to the last ulp
+    ml = engine.Model.synthetic(ctx, "linear", 1, 500, d, data_seed=seed)
+    got = ml.copy_data(0)
+    X = orc.gen_x(seed, 0, 500, d)
+    np.testing.assert_array_equal(got["x"], X)
+    np.testing.assert_allclose(got["y"], orc.gen_y_linear(seed, 0, X, 0.0, beta), rtol=1e-13, atol=1e-13)
+
+
+# ---------------------------------------------------------------- combine
+@pytest.mark.parametrize("P", [11, 53, 102])
+def test_combine_matches_reference_fixture(ctx, golden, P):
+    from stark_amd import engine
+    from stark_amd.stark import consensus_avg
+    g = golden("combine_ref.npz")
+    f1, f2 = g[f"P{P}_f1"], g[f"P{P}_f2"]
+    sw, swt = consensus_avg(2)(f1, f2)
+    cond = np.linalg.cond(g[f"P{P}_sumW"])
+    tol = 1e-12 * cond
+    assert np.abs(sw - g[f"P{P}_sumW"]).max() <= tol * np.abs(g[f"P{P}_sumW"]).max()
+    assert np.abs(swt - g[f"P{P}_sumWtheta"]).max() <= tol * np.abs(g[f"P{P}_sumWtheta"]).max()
+    out, used = engine.consensus([f1, f2], ctx)
+    assert used.all()
+    ref = g[f"P{P}_final"]
+    assert np.abs(out - ref).max() <= tol * np.abs(ref).max(), (np.abs(out - ref).max(), cond)
+
+
+def test_combine_nan_guard(ctx, golden):
+    from stark_amd import engine
+    from stark_amd.stark import consensus_avg
+    g = golden("combine_ref.npz")
+    out = consensus_avg(2)(g["nan_f1"], g["nan_f2"])
+    np.testing.assert_array_equal(out, g["nan_f2"])        # reference: NaN in f1 returns f2
+    comb, used = engine.consensus([g["nan_f1"], g["nan_f2"]], ctx)
+    assert list(used) == [False, True]
+    np.testing.assert_allclose(comb, g["nan_f2"], rtol=1e-9, atol=1e-9)   # only shard 2 left
+
+
+@pytest.mark.parametrize("S", [1, 3, 8])
+def test_combine_general_shards(ctx, orc, S):
+    from stark_amd import engine
+    from stark_amd.stark import consensus_avg
+    import functools
+    rng = np.random.default_rng(S)
+    P, n = 13, 400
+    draws = []
+    for s in range(S):
+        A = rng.normal(size=(P, P)) / np.sqrt(P)
+        L = np.linalg.cholesky(A @ A.T + 0.5 * np.eye(P))
+        draws.append(rng.normal(size=(P, 1)) + L @ rng.normal(size=(P, n)))
+    ref = orc.consensus_combine_ref(draws)
+    out, used = engine.consensus(draws, ctx)
+    assert used.all()
+    np.testing.assert_allclose(out, ref, rtol=1e-10, atol=1e-11 * np.abs(ref).max())
+    if S > 1:   # reducer chaining (functools.reduce over partitions, the reference's rdd.reduce)
+        red = functools.reduce(consensus_avg(S), draws)
+        np.testing.assert_allclose(engine.consensus_solve(red[0], red[1], ctx), ref, rtol=1e-10,
+                                   atol=1e-11 * np.abs(ref).max())
+
+
+def test_combine_singular_raises(ctx):
+    from stark_amd import engine
+    from stark_amd._lib import LinAlgError
+    x = np.ones((3, 50))
+    with pytest.raises(LinAlgError):
+        engine.consensus([x, x + 1], ctx)

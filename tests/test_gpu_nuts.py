@@ -1,0 +1,203 @@
+"""GPU NUTS (iterative per-chain state machine) vs the oracle's recursive Stan 2.19 twin,
+exact posterior moments, and reproducibility across runs / shard placements."""
+import numpy as np
+import pytest
+
+from stark_amd.diagnostics import ess
+
+pytestmark = pytest.mark.gpu
+
+
+def _schools_model(ctx, orc):
+    from stark_amd import engine
+    shards = [{"y": orc.SCHOOLS_Y[:4], "sigma": orc.SCHOOLS_SIGMA[:4]},
+              {"y": orc.SCHOOLS_Y, "sigma": orc.SCHOOLS_SIGMA}]
+    return engine.Model(ctx, "schools", shards), shards
+
+
+# ---------------------------------------------------------------- one transition, same RNG stream
+@pytest.mark.parametrize("eps", [0.05, 0.3, 0.9, 2.5])
+def test_transition_matches_oracle_schools(ctx, orc, eps):
+    m, shards = _schools_model(ctx, orc)
+    rng = np.random.default_rng(int(eps * 100))
+    C = 8
+    for shard in (0, 1):
+        om = orc.Model(orc.FAM_SCHOOLS, y=shards[shard]["y"], sigma=shards[shard]["sigma"])
+        q0 = rng.normal(0, 1, (C, om.D))
+        im = rng.uniform(0.5, 2.0, om.D)
+        q, lp, st = m.transition(shard, q0, seed=77, iteration=5, eps=eps, inv_metric=im)
+        for c in range(C):
+            oq, olp, ost, _ = om.transition(q0[c], seed=77, gid=shard * C + c, iteration=5, eps=eps, inv_metric=im)
+            np.testing.assert_allclose(q[c], oq, rtol=1e-9, atol=1e-10)
+            assert abs(lp[c] - olp) <= 1e-9 * max(1, abs(olp))
+            assert st[c, 2] == ost[2] and st[c, 3] == ost[3] and st[c, 4] == ost[4], (c, st[c], ost)
+            np.testing.assert_allclose(st[c, [0, 5]], ost[[0, 5]], rtol=1e-9, atol=1e-12)
+
+
+def test_transition_matches_oracle_logistic(ctx, orc):
+    from stark_amd import engine
+    rng = np.random.default_rng(4)
+    n, d = 400, 6
+    X = rng.uniform(-1.7, 1.7, (n, d))
+    y = (rng.uniform(size=n) < 1 / (1 + np.exp(-X @ rng.normal(0, 0.5, d)))).astype(np.int32)
+    m = engine.Model(ctx, "logistic", [{"x": X, "y": y}])
+    om = orc.Model(orc.FAM_LOGREG, X=X, y=y)
+    C = 4
+    q0 = rng.normal(0, 0.1, (C, d + 1))
+    q, lp, st = m.transition(0, q0, seed=3, iteration=11, eps=0.08)
+    for c in range(C):
+        oq, olp, ost, _ = om.transition(q0[c], seed=3, gid=c, iteration=11, eps=0.08)
+        np.testing.assert_allclose(q[c], oq, rtol=1e-8, atol=1e-10)
+        assert st[c, 3] == ost[3]
+
+
+# ---------------------------------------------------------------- adaptive run vs oracle twin
+def test_adaptive_run_tracks_oracle(ctx, orc):
+    """Full warmup (init_stepsize probes, dual averaging, Welford windows) on the GPU and the
+    oracle from the same seed: the chains follow the same path."""
+    m, shards = _schools_model(ctx, orc)
+    nw, ns, C = 150, 30, 2
+    res = m.sampler(num_warmup=nw, num_samples=ns, chains=C, seed=2024)
+    res.run()
+    eps, im = res.adaptation()
+    for shard in (0, 1):
+        om = orc.Model(orc.FAM_SCHOOLS, y=shards[shard]["y"], sigma=shards[shard]["sigma"])
+        uq = res.unconstrained(shard)
+        for c in range(C):
+            o = om.run_chain(num_warmup=nw, num_samples=ns, seed=2024, gid=shard * C + c)
+            g = shard * C + c
+            np.testing.assert_allclose(eps[g], o["stepsize"], rtol=1e-8)
+            np.testing.assert_allclose(im[g, :om.D], o["inv_metric"], rtol=1e-8)
+            np.testing.assert_allclose(uq[c], o["q"][nw:], rtol=1e-7, atol=1e-8)
+    res.close()
+
+
+# ---------------------------------------------------------------- statistics
+def test_schools_4096_chains_exact_moments(ctx, orc):
+    """BASELINE config 2: 8 schools with 4096 parallel chains on one GPU."""
+    from stark_amd import engine
+    m = engine.Model(ctx, "schools", [{"y": orc.SCHOOLS_Y, "sigma": orc.SCHOOLS_SIGMA}])
+    C = 4096
+    s = m.sampler(num_warmup=500, num_samples=200, chains=C, seed=7)
+    s.run()
+    info = s.info()
+    assert info["errors"] == 0 and info["done"] == C
+    uq = s.unconstrained(0)          # C x 200 x 10
+    em, ev = orc.schools_exact_moments(orc.SCHOOLS_Y, orc.SCHOOLS_SIGMA)
+    for k in range(10):
+        x = uq[:, :, k]
+        e = ess(x)
+        mcse = x.std() / np.sqrt(e)
+        assert abs(x.mean() - em[k]) < 5 * mcse, (k, x.mean(), em[k], mcse, e)
+    np.testing.assert_allclose(uq[:, :, 2:].reshape(-1, 8).var(0), ev[2:], rtol=0.05)
+    d, st = s.draws(0)
+    assert d.shape == (19, C * 200)
+    np.testing.assert_allclose(d[1], np.exp(uq[:, :, 1].reshape(-1)), rtol=1e-15)        # tau
+    np.testing.assert_allclose(d[10], d[0] + d[1] * d[2], rtol=1e-12, atol=1e-12)        # theta[1]
+    assert 0.7 < st[:, 0].mean() < 0.95
+    s.close()
+
+
+def test_linear_regression_closed_form(ctx, orc):
+    from stark_amd import engine
+    rng = np.random.default_rng(8)
+    n, d = 2000, 5
+    X = rng.uniform(-1.7, 1.7, (n, d))
+    y = 0.7 + X @ rng.normal(0, 0.5, d) + 1.3 * rng.normal(size=n)
+    m = engine.Model(ctx, "linear", [{"x": X, "y": y}])
+    C = 8
+    s = m.sampler(num_warmup=500, num_samples=1000, chains=C, seed=21)
+    s.run()
+    uq = s.unconstrained(0)
+    mean, cov = orc.linreg_exact_moments(X, y)
+    sd = np.sqrt(np.diag(cov))
+    for k in range(d + 1):
+        x = uq[:, :, k]
+        mcse = x.std() / np.sqrt(ess(x))
+        assert abs(x.mean() - mean[k]) < 5 * mcse, (k, x.mean(), mean[k], mcse)
+        assert abs(x.std() / sd[k] - 1) < 0.06
+    s.close()
+
+
+def test_logistic_matches_oracle_moments(ctx, orc):
+    from stark_amd import engine
+    rng = np.random.default_rng(12)
+    n, d = 3000, 4
+    X = rng.uniform(-1.7, 1.7, (n, d))
+    y = (rng.uniform(size=n) < 1 / (1 + np.exp(-(0.2 + X @ rng.normal(0, 0.6, d))))).astype(np.int32)
+    m = engine.Model(ctx, "logistic", [{"x": X, "y": y}])
+    s = m.sampler(num_warmup=500, num_samples=1000, chains=8, seed=5)
+    s.run()
+    g = s.unconstrained(0)
+    om = orc.Model(orc.FAM_LOGREG, X=X, y=y)
+    runs = [om.run_chain(num_warmup=500, num_samples=1000, seed=99, gid=c) for c in range(4)]
+    o = np.stack([r["q"][500:] for r in runs])
+    for k in range(d + 1):
+        a, b = g[:, :, k], o[:, :, k]
+        se = np.hypot(a.std() / np.sqrt(ess(a)), b.std() / np.sqrt(ess(b)))
+        assert abs(a.mean() - b.mean()) < 5 * se, (k, a.mean(), b.mean(), se)
+        assert abs(a.std() / b.std() - 1) < 0.1
+    s.close()
+
+
+# ---------------------------------------------------------------- reproducibility
+def test_bitwise_reproducible_and_resumable(ctx):
+    from stark_amd import engine
+    m = engine.Model.synthetic(ctx, "logistic", 2, 5000, 8, data_seed=3)
+    cfg = dict(num_warmup=60, num_samples=40, chains=2, seed=11)
+    a = m.sampler(**cfg)
+    a.run()
+    b = m.sampler(**cfg)
+    b.run(30)
+    b.run(75)
+    b.run()
+    for s in range(2):
+        np.testing.assert_array_equal(a.draws(s)[0], b.draws(s)[0])
+    ia, ib = a.info(), b.info()
+    assert ia["grad_evals"] == ib["grad_evals"] and ia["leapfrogs"] == ib["leapfrogs"]
+    a.close()
+    b.close()
+
+
+def test_shard_placement_independent(ctx):
+    """1 GPU holding 4 shards == 4 GPUs holding one shard each (same global shard ids)."""
+    from stark_amd import engine
+    rows, d = 3000, 10
+    cfg = dict(num_warmup=50, num_samples=30, chains=4, seed=5)
+    full = engine.Model.synthetic(ctx, "logistic", 4, rows, d, data_seed=8)
+    ref = full.sample(**cfg)
+    for k in (1, 3):
+        one = engine.Model.synthetic(ctx, "logistic", 1, rows, d, data_seed=8, row_offset=k * rows)
+        r = one.sample(shard_ids=[k], **cfg)
+        np.testing.assert_array_equal(r.draws[0], ref.draws[k])
+        one.close()
+    full.close()
+
+
+def test_stark_api_schools_end_to_end(ctx):
+    import os
+    from conftest import ROOT
+    from stark_amd import stark
+    from stark_amd.rdd import LocalContext
+    sc = LocalContext()
+    school = list(zip([28, 8, -3, 7, -1, 1, 18, 12], [15, 10, 16, 11, 9, 11, 10, 18]))
+
+    def prep(data):
+        return {"J": len(data), "y": [d[0] for d in data], "sigma": [d[1] for d in data]}
+
+    st = stark.Stark(sc, sc.parallelize(school, 2), prep)
+    st.setStanModel(file=os.path.join(ROOT, "stark_amd", "models", "schools.stan"))
+    w = st.concensusWeight(iter=1000, seed=3)
+    assert w.shape == (11, 500) and np.all(np.isfinite(w))
+    nv = st.distribute(n=2, iter=400, seed=4)
+    assert nv.shape == (38, 200)
+
+
+def test_driver_weighted_matches_reference(ctx, golden, monkeypatch):
+    """concensusWeight orchestration + GPU combine vs the reference driver on the same fake fits."""
+    import test_host
+    st = test_host._fake_stark(monkeypatch)
+    g = golden("driver_ref.npz")
+    out = st.concensusWeight(iter=600)
+    ref = g["weighted"]
+    np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-10 * np.abs(ref).max())

@@ -1,0 +1,187 @@
+"""Host-side logic (CPU only): the C-ABI library, Stan front end, RDD shim, driver
+orchestration against the reference's own driver outputs, diagnostics."""
+import collections
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+# ---------------------------------------------------------------- C ABI
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "stark_hip.h")).read()
+    return sorted(set(re.findall(r"STK_API\s+[\w\s\*]+?\b(stk_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    import ctypes
+    from stark_amd import _lib
+    lib = _lib.load()
+    names = _header_symbols()
+    assert len(names) >= 25
+    for n in names:
+        assert hasattr(lib, n), n
+    bound = {s[0] for s in _lib.SIGNATURES}
+    assert set(names) == bound, set(names) ^ bound
+    assert lib.stk_version() == 1
+    c = _lib.default_config()
+    assert (c.num_warmup, c.num_samples, c.chains, c.max_depth) == (1000, 1000, 1, 10)
+    assert c.adapt_delta == 0.8 and c.stepsize == 1.0 and c.adapt_init_buffer == 75
+    # struct layouts must match the C header: compile a probe with gcc
+    import subprocess, tempfile
+    src = ('#include <stdio.h>\n#include <stddef.h>\n#include "stark_hip.h"\n'
+           'int main(){printf("%zu %zu %zu %zu %zu", sizeof(stk_config), sizeof(stk_shard), sizeof(stk_run_info),'
+           ' offsetof(stk_config, seed), offsetof(stk_config, shard_ids));return 0;}')
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "p.c"), "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", os.path.join(d, "p"), os.path.join(d, "p.c")],
+                       check=True)
+        got = [int(v) for v in subprocess.run([os.path.join(d, "p")], capture_output=True, text=True).stdout.split()]
+    assert got == [ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.Shard), ctypes.sizeof(_lib.RunInfo),
+                   _lib.Config.seed.offset, _lib.Config.shard_ids.offset]
+
+
+def test_no_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from stark_amd import engine
+    from stark_amd._lib import StarkHipError
+    with pytest.raises(StarkHipError):
+        engine.Context(0)
+
+
+# ---------------------------------------------------------------- front end
+def test_recognise_programs():
+    from stark_amd import frontend
+    for fam in ("schools", "logistic", "linear"):
+        code = open(os.path.join(ROOT, "stark_amd", "models", f"{fam}.stan")).read()
+        assert frontend.recognise(code) == fam
+    newsyntax = """
+    data { int<lower=0> J; array[J] real y; array[J] real<lower=0> sigma; }
+    parameters { real mu; real<lower=0> tau; vector[J] eta; }
+    transformed parameters { vector[J] theta = mu + tau * eta; }
+    model { eta ~ std_normal(); y ~ normal(theta, sigma); }"""
+    assert frontend.recognise(newsyntax) == "schools"
+    with pytest.raises(NotImplementedError):
+        frontend.recognise(newsyntax.replace("std_normal()", "normal(0, 2)"))
+    prior = open(os.path.join(ROOT, "stark_amd", "models", "logistic.stan")).read().replace(
+        "model {", "model {\n beta ~ normal(0, 1);")
+    with pytest.raises(NotImplementedError):
+        frontend.recognise(prior)
+
+
+def test_pack_data_validation():
+    from stark_amd import frontend
+    d = frontend.pack_data("schools", {"J": 2, "y": [1, 2], "sigma": [3, 4]})
+    assert d["y"].dtype == np.float64
+    with pytest.raises(ValueError):
+        frontend.pack_data("schools", {"J": 3, "y": [1, 2], "sigma": [3, 4]})
+    with pytest.raises(ValueError):
+        frontend.pack_data("schools", {"J": 2, "y": [1, 2], "sigma": [3, 0]})
+    r = frontend.pack_data("logistic", {"N": 2, "K": 1, "x": [[1.0], [2.0]], "y": [0, 1]})
+    assert r["y"].dtype == np.int32 and r["x"].shape == (2, 1)
+    assert frontend.column_names("schools", {"J": 2}) == ["mu", "tau", "eta[1]", "eta[2]", "theta[1]", "theta[2]",
+                                                          "lp__"]
+
+
+def test_sampling_config_mapping():
+    from stark_amd.stark import sampling_config
+    datas = [{"J": 4, "y": [1, 2, 3, 4], "sigma": [1, 1, 1, 1]}]
+    c = sampling_config("schools", datas, iter=5000, chains=1, n_jobs=1, seed=9,
+                        control={"adapt_delta": 0.9, "max_treedepth": 12})
+    assert c["num_warmup"] == 2500 and c["num_samples"] == 2500
+    assert c["adapt_delta"] == 0.9 and c["max_depth"] == 12 and c["seed"] == 9
+    c0 = sampling_config("schools", datas, iter=20, chains=2, init=0, seed=1)
+    assert c0["init"].shape == (12,) and not c0["init"].any()
+    ci = sampling_config("schools", datas, iter=20, chains=1, seed=1, init=[{"mu": 1.0, "tau": np.e}])
+    assert ci["init"][0] == 1.0 and abs(ci["init"][1] - 1.0) < 1e-15
+    with pytest.raises(NotImplementedError):
+        sampling_config("schools", datas, thin=2)
+    with pytest.raises(TypeError):
+        sampling_config("schools", datas, bogus=1)
+
+
+# ---------------------------------------------------------------- RDD shim
+def test_local_rdd_semantics():
+    from stark_amd.rdd import LocalContext
+    sc = LocalContext()
+    school = list(zip([28, 8, -3, 7, -1, 1, 18, 12], [15, 10, 16, 11, 9, 11, 10, 18]))
+    rdd = sc.parallelize(school, 2)
+    assert rdd.getNumPartitions() == 2
+    assert rdd.partitions()[0] == school[:4] and rdd.partitions()[1] == school[4:]
+    assert [len(p) for p in sc.parallelize(range(8), 3).partitions()] == [2, 3, 3]   # Spark slicing
+    assert rdd.coalesce(1).partitions() == [school]
+    assert rdd.union(rdd.coalesce(1)).getNumPartitions() == 3
+    assert sc.parallelize(range(5), 2).reduce(lambda a, b: a * 10 + b) == 1234
+
+
+# ---------------------------------------------------------------- driver vs reference driver (fake sampler)
+def _fake_extract(data, it, chains=1):
+    """Same fake fit as tests/golden/make_golden.py's FakeStanModel."""
+    J = data["J"]
+    S = it // 2 * chains
+    seed = int(abs(sum(data["y"]) * 1000 + sum(data["sigma"]))) % (2 ** 32)
+    rng = np.random.default_rng(seed)
+    mu = rng.normal(8, 5, S)
+    tau = np.exp(rng.normal(1.5, 1.0, S))
+    eta = rng.normal(0, 1, (S, J))
+    theta = mu[:, None] + tau[:, None] * eta
+    lp = rng.normal(-40, 3, S)
+    return collections.OrderedDict([("mu", mu), ("tau", tau), ("eta", eta), ("theta", theta), ("lp__", lp)])
+
+
+def prepare_school_data(data):
+    return {"J": len(data), "y": [d[0] for d in data], "sigma": [d[1] for d in data]}
+
+
+def _fake_stark(monkeypatch):
+    from stark_amd import stark as S
+    from stark_amd.rdd import LocalContext
+
+    def fake(self, datas, **kw):
+        return [S._extract_to_matrix(_fake_extract(d, kw["iter"], kw.get("chains", 1))) for d in datas]
+
+    monkeypatch.setattr(S.Stark, "_sample_partitions", fake)
+    sc = LocalContext()
+    school = list(zip([28, 8, -3, 7, -1, 1, 18, 12], [15, 10, 16, 11, 9, 11, 10, 18]))
+    st = S.Stark(sc, sc.parallelize(school, 2), prepare_school_data)
+    st.setStanModel(file=os.path.join(ROOT, "stark_amd", "models", "schools.stan"))
+    return st
+
+
+def test_driver_mcmc_closure_matches_reference(golden, monkeypatch):
+    st = _fake_stark(monkeypatch)
+    g = golden("driver_ref.npz")
+    school = list(zip([28, 8, -3, 7, -1, 1, 18, 12], [15, 10, 16, 11, 9, 11, 10, 18]))
+    w = st._mcmc(prepare_school_data, iter=2000, chains=1, n_jobs=1)
+    np.testing.assert_array_equal(w(iter(school[:4]))[0], g["part0"])
+
+
+def test_driver_distribute_reference_union(golden, monkeypatch):
+    st = _fake_stark(monkeypatch)
+    g = golden("driver_ref.npz")
+    out = st.distribute(n=4, iter=200, reference_union=True)
+    assert out.shape == (41, 100)
+    np.testing.assert_array_equal(out, g["naive"])
+    intent = st.distribute(n=4, iter=200)
+    assert intent.shape == (4 * 19, 100)
+
+
+# ---------------------------------------------------------------- diagnostics
+def test_ess_ar1():
+    from stark_amd.diagnostics import ess, split_rhat
+    rng = np.random.default_rng(0)
+    rho, n, nc = 0.6, 20000, 4
+    x = np.zeros((nc, n))
+    e = rng.normal(size=(nc, n))
+    for t in range(1, n):
+        x[:, t] = rho * x[:, t - 1] + e[:, t]
+    want = nc * n * (1 - rho) / (1 + rho)
+    assert abs(ess(x) / want - 1) < 0.1
+    assert abs(split_rhat(x) - 1) < 0.01
+    iid = rng.normal(size=(4, 5000))
+    assert abs(ess(iid) / 20000 - 1) < 0.1
