@@ -111,10 +111,21 @@ def main():
     A, W, K = a.adapt_iters, a.warmup, a.steps
     sampler = model.sampler(num_warmup=A, num_samples=W + K, chains=a.chains, seed=a.seed + 1,
                             shard_ids=shard_ids)
+    def log(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    log(f"data generated: {spr} shards x {rows_per_shard} rows x d={a.d} in {t_gen:.1f}s "
+        f"({model.device_bytes() / 1e9:.1f} GB on this GPU)")
     t = time.perf_counter()
-    sampler.run(A)
+    for it in range(10, A + 10, 10):
+        sampler.run(min(it, A))
+        inf = sampler.info()
+        log(f"adaptation {min(it, A)}/{A}: {time.perf_counter() - t:.1f}s, leapfrogs/chain "
+            f"{inf['leapfrogs'] / max(1, spr * a.chains):.0f}")
     t_adapt = time.perf_counter() - t
     sampler.run(A + W)
+    log(f"warmup steps done; timing {K} steps")
 
     def barrier():
         torch.cuda.synchronize(local_rank)

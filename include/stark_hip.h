@@ -90,6 +90,8 @@ typedef struct {
   const double* inv_metric;  /* NULL (unit), or D initial diagonal inverse metric */
   int32_t skip_init_stepsize;/* test hook: do not run base_hmc::init_stepsize */
   int32_t iter_offset;       /* test hook: RNG iteration index of the first transition */
+  int32_t save_warmup;       /* also keep unconstrained warmup draws (pystan inc_warmup):
+                                stk_sampler_draws_unconstrained then returns all iterations */
   const int32_t* shard_ids;  /* NULL, or the GLOBAL index of every local shard: chain c of shard s
                                 draws from RNG stream shard_ids[s] * chains + c, so a shard samples
                                 identically whichever GPU (and with whichever other shards) it runs */
@@ -146,7 +148,8 @@ STK_API int stk_sampler_info(stk_sampler* s, stk_run_info* info);
  * [chains * num_samples][6] = accept_stat, stepsize, treedepth, n_leapfrog, divergent, energy.
  * Either pointer may be NULL. */
 STK_API int stk_sampler_draws(stk_sampler* s, int shard, double* out, double* stats);
-/* Unconstrained draws of one shard: out[chains][num_samples][D]. */
+/* Unconstrained draws of one shard: out[chains][num_samples][D], or
+ * out[chains][num_warmup + num_samples][D] when cfg.save_warmup is set. */
 STK_API int stk_sampler_draws_unconstrained(stk_sampler* s, int shard, double* out);
 STK_API int stk_sampler_adaptation(stk_sampler* s, double* stepsize, double* inv_metric);
 STK_API int stk_sampler_destroy(stk_sampler* s);

@@ -90,14 +90,18 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// Handles are reference counted (a model holds its context, a sampler its model), so the
+// caller may destroy them in any order -- e.g. a garbage collector finalising a cycle.
 struct stk_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int profiling = 0;
+  int refs = 1;
   DevBuf scratch[8];
 };
 
 struct stk_model {
+  int refs = 1;
   stk_ctx* ctx = nullptr;
   int family = 0;
   int nshards = 0;
@@ -172,13 +176,17 @@ int stk_ctx_create(int device, stk_ctx** out) {
   return STK_OK;
 }
 
-int stk_ctx_destroy(stk_ctx* c) {
-  if (!c) return STK_OK;
+static void ctx_release(stk_ctx* c) {
+  if (--c->refs > 0) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   for (auto& b : c->scratch) b.release();
   hipStreamDestroy(c->stream);
   delete c;
+}
+
+int stk_ctx_destroy(stk_ctx* c) {
+  if (c) ctx_release(c);
   return STK_OK;
 }
 
@@ -237,6 +245,7 @@ int stk_model_create(stk_ctx* ctx, int family, const stk_shard* shards, int nsha
   STK_HIP_CHECK(hipSetDevice(ctx->device));
   stk_model* m = new stk_model();
   m->ctx = ctx;
+  ctx->refs++;
   m->family = family;
   m->nshards = nshards;
   m->d = family == STK_SCHOOLS ? 0 : shards[0].n_cols;
@@ -306,6 +315,7 @@ int stk_model_create_synthetic(stk_ctx* ctx, int family, int nshards, int64_t ro
   else stk_gen_beta(data_seed, n_cols, b.data());
   stk_model* m = new stk_model();
   m->ctx = ctx;
+  ctx->refs++;
   m->family = family;
   m->nshards = nshards;
   m->d = n_cols;
@@ -349,13 +359,19 @@ int stk_model_create_synthetic(stk_ctx* ctx, int family, int nshards, int64_t ro
   return STK_OK;
 }
 
-int stk_model_destroy(stk_model* m) {
-  if (!m) return STK_OK;
-  hipSetDevice(m->ctx->device);
-  hipStreamSynchronize(m->ctx->stream);
+static void model_release(stk_model* m) {
+  if (--m->refs > 0) return;
+  stk_ctx* c = m->ctx;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
   for (auto& b : m->bufs) b.release();
   m->sh_dev.release();
   delete m;
+  ctx_release(c);
+}
+
+int stk_model_destroy(stk_model* m) {
+  if (m) model_release(m);
   return STK_OK;
 }
 
@@ -454,8 +470,9 @@ static int sbuf(stk_sampler* s, size_t bytes, void** p) {
 
 int stk_sampler_destroy(stk_sampler* s) {
   if (!s) return STK_OK;
-  hipSetDevice(s->m->ctx->device);
-  hipStreamSynchronize(s->m->ctx->stream);
+  stk_model* m = s->m;
+  hipSetDevice(m->ctx->device);
+  hipStreamSynchronize(m->ctx->stream);
   for (auto& b : s->bufs) b.release();
   s->partial.release();
   s->lp.release();
@@ -463,6 +480,7 @@ int stk_sampler_destroy(stk_sampler* s) {
   s->ran.release();
   for (auto e : s->ev) hipEventDestroy(e);
   delete s;
+  model_release(m);
   return STK_OK;
 }
 
@@ -480,6 +498,7 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   else ARG_CHECK(stk_sweep_supported(cfg->chains, m->d), "chains per shard must be 1, 2, 4 or 8 for regressions");
   stk_sampler* s = new stk_sampler();
   s->m = m;
+  m->refs++;
   s->cfg = *cfg;
   s->nch = nch;
   NutsArgs& A = s->A;
@@ -530,7 +549,9 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   ALLOC(g_in, double, (size_t)nchains * Dp);
   ALLOC(draws, double, (size_t)m->nshards * m->Pmax * A.S_total);
   ALLOC(stats, double, (size_t)m->nshards * A.S_total * N_STATS);
-  ALLOC(udraws, double, (size_t)nchains * cfg->num_samples * Dp);
+  A.ud_first = cfg->save_warmup ? 0 : cfg->num_warmup;
+  A.ud_iters = A.total_iters - A.ud_first;
+  ALLOC(udraws, double, (size_t)nchains * A.ud_iters * Dp);
   ALLOC(req_step, int, (size_t)m->nshards);
 #undef ALLOC
   double* init_dev = nullptr;
@@ -757,7 +778,7 @@ int stk_sampler_draws_unconstrained(stk_sampler* s, int shard, double* out) {
   stk_ctx* ctx = s->m->ctx;
   STK_HIP_CHECK(hipSetDevice(ctx->device));
   const int D = s->m->sh[shard].D;
-  const size_t rows = (size_t)s->A.C * s->A.num_samples;
+  const size_t rows = (size_t)s->A.C * s->A.ud_iters;
   const double* src = s->A.udraws + (size_t)shard * rows * s->A.Dp;
   STK_HIP_CHECK(hipMemcpy2DAsync(out, sizeof(double) * D, src, sizeof(double) * s->A.Dp, sizeof(double) * D, rows,
                                  hipMemcpyDefault, ctx->stream));

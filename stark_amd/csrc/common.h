@@ -9,6 +9,24 @@ namespace stk {
 
 constexpr int WAVE = 64;
 
+// Pointers fetched from device structs are generic to the compiler: loads through them
+// become flat_load (counted on both vmcnt and lgkmcnt, so every LDS wait drains them).
+// Casting to the global address space restores global_load with independent counters.
+template <class T>
+using gptr_t = const __attribute__((address_space(1))) T*;
+template <class T>
+__device__ __forceinline__ gptr_t<T> gp(const T* p) { return (gptr_t<T>)p; }
+
+// Read-only data at wave-uniform addresses through the constant address space: the
+// compiler emits scalar loads (s_load, lgkmcnt) that never wait on in-flight vector loads.
+template <class T>
+using cptr_t = const __attribute__((address_space(4))) T*;
+template <class T>
+__device__ __forceinline__ cptr_t<T> cp(const T* p) { return (cptr_t<T>)p; }
+
+// A value the compiler cannot prove wave-uniform (e.g. threadIdx.x >> 6), made uniform.
+__device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 // One data shard resident in HBM (copied or generated once, then streamed every sweep).
 struct ShardDev {
   const double* x;      // n x d row-major (regressions)
@@ -66,7 +84,9 @@ struct NutsArgs {
   double* g_in;     // nchains * Dp   grad lp at the requested points
   double* draws;    // nshards * Pmax * S_total   (P x S per shard, chain-major columns)
   double* stats;    // nshards * S_total * N_STATS
-  double* udraws;   // nchains * num_samples * Dp
+  double* udraws;   // nchains * ud_iters * Dp  (unconstrained draws)
+  int ud_first;     // first transition index stored in udraws (num_warmup, or 0 with save_warmup)
+  int ud_iters;     // transitions stored per chain
   int* req_step;    // nshards: last step index that issued a request for the shard
   const int* shard_ids;  // nullptr or global shard index per local shard (RNG stream keys)
 };

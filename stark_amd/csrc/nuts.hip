@@ -340,13 +340,16 @@ struct NutsChain {
   __device__ bool end_transition(int pause_at) {
     const double accept = s[S_SUMMETRO] / (double)iv[I_NLEAP];
     const int it = iv[I_ITER];
+    if (it >= A.ud_first) {
+      double qs[NCH];
+      ld(vp(V_QS), qs);
+      st(A.udraws + ((size_t)gid * A.ud_iters + (it - A.ud_first)) * A.Dp, qs);
+    }
     if (it >= A.num_warmup) {
       const int col = cidx * A.num_samples + (it - A.num_warmup);
       double qs[NCH];
       ld(vp(V_QS), qs);
       write_draw<NCH>(A, sh, shard, col, qs, -s[S_VS], lane);
-      double* ud = A.udraws + ((size_t)gid * A.num_samples + (it - A.num_warmup)) * A.Dp;
-      st(ud, qs);
       if (lane < N_STATS) {
         double v = 0;
         switch (lane) {

@@ -17,9 +17,13 @@
 // results are bitwise independent of how many shards share a GPU.
 #include "common.h"
 #include <math.h>
+#include <stdlib.h>
+#include <algorithm>
 #include <type_traits>
 
 namespace stk {
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));   // loads from any address space
 
 struct SweepArgs {
   const ShardDev* shards;
@@ -78,14 +82,14 @@ __global__ __launch_bounds__(256) void k_sweep(SweepArgs A) {
   const int fr = tid / S, fs = tid % S;   // forward mapping
 
   // tile staging: VEC doubles per load, element e = VEC*(tid + NT*v) of the tile
-  using vec_t = typename std::conditional<VEC == 2, double2, double>::type;
+  using vec_t = typename std::conditional<VEC == 2, dbl2, double>::type;
   vec_t buf[NVMAX];
   const int64_t ntiles = (r1 - r0 + T - 1) / T;
   auto prefetch = [&](int64_t t) {
     const int64_t row_start = r0 + t * T;
     const int64_t rows = (r1 - row_start) < T ? (r1 - row_start) : T;
     const int64_t nel = rows * d;
-    const vec_t* src = reinterpret_cast<const vec_t*>(sh.x + row_start * d);
+    const gptr_t<vec_t> src = (gptr_t<vec_t>)(gp(sh.x) + row_start * d);
 #pragma unroll
     for (int v = 0; v < NVMAX; ++v) {
       const int64_t e = (int64_t)VEC * (tid + NT * v);
@@ -103,7 +107,7 @@ __global__ __launch_bounds__(256) void k_sweep(SweepArgs A) {
     for (int v = 0; v < NVMAX; ++v) {
       if (e < nel) {
         if constexpr (VEC == 2) {
-          *reinterpret_cast<double2*>(&Xs[row * LD + col]) = buf[v];
+          *reinterpret_cast<dbl2*>(&Xs[row * LD + col]) = buf[v];
         } else {
           Xs[row * LD + col] = buf[v];
         }
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(256) void k_sweep(SweepArgs A) {
           const int64_t row = row_start + fr;
           const double eta = Al[c] + acc[c];
           if constexpr (FAM == STK_LOGREG) {
-            const double sgn = 2.0 * sh.yi[row] - 1.0;
+            const double sgn = 2.0 * gp(sh.yi)[row] - 1.0;
             const double nt = sgn * eta;
             const double e = exp(-nt);
             if (nt > 20.0) { lpa[c] -= e; de = sgn * e; }
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(256) void k_sweep(SweepArgs A) {
             else { lpa[c] -= log1p(e); de = sgn * e / (e + 1.0); }
           } else {
             const double is = Al[C + c];
-            const double z = (sh.y[row] - eta) * is;
+            const double z = (gp(sh.y)[row] - eta) * is;
             lpa[c] += z * z;          // linreg: sum of squares, finished in the reduce
             de = z * is;
           }
@@ -217,6 +221,193 @@ __global__ __launch_bounds__(256) void k_sweep(SweepArgs A) {
   }
 }
 
+// v2 sweep for d <= 128 (T = 64-row tiles, 4 waves):
+//   forward   wave w owns columns [w*d/4, (w+1)*d/4), lane = row: eta partials with beta_c[j]
+//             as wave-uniform (scalar) operands -- one LDS read per 64 rows per column;
+//   residual  64*C (row, chain) pairs over all 256 threads (full lanes for exp/log1p);
+//   backward  wave w owns rows [16w, 16w+16), lane = column (JPT = 2), residuals broadcast.
+// LDS row stride LD is odd, so lane-per-row reads and lane-per-column reads are both free of
+// bank conflicts; tiles are register-prefetched one ahead (global_load_dwordx4).
+template <int FAM, int C>
+__global__ __launch_bounds__(256, 2) void k_sweep2(SweepArgs A) {
+  constexpr int T = 64, NT = 256, JPT = 2;
+  constexpr int CP = (T * C + NT - 1) / NT;       // residual pairs per thread
+  constexpr int NVMAX = (T * 128 / 2 + NT - 1) / NT;
+  using yv_t = typename std::conditional<FAM == STK_LOGREG, int32_t, double>::type;
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d, LD = A.LD, tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int64_t r0 = sh.n * chunk / A.G, r1 = sh.n * (chunk + 1) / A.G;
+  const cptr_t<double> qs = cp(A.q) + (size_t)shard * C * A.Dp;   // chain c: (alpha, beta, [u])
+  const gptr_t<double> X = gp(sh.x);
+  const gptr_t<yv_t> Y = (gptr_t<yv_t>)(FAM == STK_LOGREG ? (const void*)sh.yi : (const void*)sh.y);
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* Xs = lds;                    // T * LD
+  double* Part = Xs + T * LD;          // [4][C][T] forward partials
+  double* Rs = Part + 4 * C * T;       // [T][C] d eta
+
+  const int jq = (d + 3) / 4;
+  const int j0 = min(d, w * jq), j1 = min(d, j0 + jq);
+  double alpha[C], inv_s[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    alpha[c] = qs[(size_t)c * A.Dp];
+    inv_s[c] = (FAM == STK_LINREG) ? exp(-qs[(size_t)c * A.Dp + d + 1]) : 0.0;
+  }
+
+  double gacc[JPT][C];
+  double lpa[CP], ga[CP];
+#pragma unroll
+  for (int i = 0; i < CP; ++i) { lpa[i] = 0.0; ga[i] = 0.0; }
+#pragma unroll
+  for (int m = 0; m < JPT; ++m)
+#pragma unroll
+    for (int c = 0; c < C; ++c) gacc[m][c] = 0.0;
+
+  dbl2 buf[NVMAX];
+  yv_t yv = 0;                         // y of row (tile start + lane): the only row this thread's residuals use
+  const int64_t ntiles = (r1 - r0 + T - 1) / T;
+  const int step = 2 * NT, dq = step / d, dr = step % d;
+  auto issue = [&](int64_t rs) {       // prefetch X tile + y values starting at row rs
+    const int64_t rws = (r1 - rs) < T ? (r1 - rs) : T;
+    const int64_t nvec = rws * d / 2;
+    const gptr_t<dbl2> src = (gptr_t<dbl2>)(X + rs * d);
+#pragma unroll
+    for (int v = 0; v < NVMAX; ++v)
+      if ((int64_t)(tid + NT * v) < nvec) buf[v] = src[tid + NT * v];
+    if (lane < rws) yv = Y[rs + lane];
+  };
+
+  if (ntiles > 0) issue(r0);
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int64_t row_start = r0 + t * T;
+    const int rows = (int)((r1 - row_start) < T ? (r1 - row_start) : T);
+    const yv_t ycur = yv;
+    {   // stage the prefetched tile into LDS (2 x ds_write_b64: LD is odd)
+      const int nel = rows * d;
+      int e = 2 * tid, row = e / d, col = e % d;
+#pragma unroll
+      for (int v = 0; v < NVMAX; ++v) {
+        if (e < nel) {
+          double* dst = Xs + row * LD + col;
+          dst[0] = buf[v].x;
+          dst[1] = buf[v].y;
+        }
+        e += step;
+        row += dq;
+        col += dr;
+        if (col >= d) { col -= d; ++row; }
+      }
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) issue(row_start + T);   // next tile in flight during this tile's compute
+    // ---- forward partials: lane = row, wave = column quarter; beta via scalar loads
+    {
+      double acc[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] = 0.0;
+      if (lane < rows) {
+        const double* xr = Xs + lane * LD;
+#pragma unroll 4
+        for (int j = j0; j < j1; ++j) {
+          const double x = xr[j];
+#pragma unroll
+          for (int c = 0; c < C; ++c) acc[c] = fma(x, qs[(size_t)c * A.Dp + 1 + j], acc[c]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) Part[(w * C + c) * T + lane] = acc[c];
+    }
+    __syncthreads();
+    // ---- residuals: pair p = tid + NT*i -> (row p%64 = lane, chain p/64)
+#pragma unroll
+    for (int i = 0; i < CP; ++i) {
+      const int p = tid + NT * i;
+      if (p < T * C) {
+        const int r = lane, c = p >> 6;
+        double de = 0.0;
+        if (r < rows) {
+          double a = alpha[0], is = inv_s[0];
+#pragma unroll
+          for (int cc = 1; cc < C; ++cc)
+            if (cc == c) { a = alpha[cc]; is = inv_s[cc]; }
+          const double eta = a + (((Part[(0 * C + c) * T + r] + Part[(1 * C + c) * T + r]) +
+                                   Part[(2 * C + c) * T + r]) + Part[(3 * C + c) * T + r]);
+          if constexpr (FAM == STK_LOGREG) {
+            const double sgn = 2.0 * ycur - 1.0;
+            const double nt = sgn * eta;
+            const double e = exp(-nt);
+            if (nt > 20.0) { lpa[i] -= e; de = sgn * e; }
+            else if (nt < -20.0) { lpa[i] += nt; de = sgn; }
+            else { lpa[i] -= log1p(e); de = sgn * e / (e + 1.0); }
+          } else {
+            const double z = (ycur - eta) * is;
+            lpa[i] += z * z;
+            de = z * is;
+          }
+          ga[i] += de;
+        }
+        Rs[r * C + c] = de;
+      }
+    }
+    __syncthreads();
+    // ---- backward: wave w owns 16 rows, lane = column
+    {
+      const int rb0 = w * (T / 4), rb1 = min(rows, rb0 + T / 4);
+      for (int r = rb0; r < rb1; ++r) {
+        double rv[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) rv[c] = Rs[r * C + c];
+        const double* xr = Xs + r * LD;
+#pragma unroll
+        for (int m = 0; m < JPT; ++m) {
+          const int j = lane + 64 * m;
+          if (j < d) {
+            const double x = xr[j];
+#pragma unroll
+            for (int c = 0; c < C; ++c) gacc[m][c] = fma(x, rv[c], gacc[m][c]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- fixed-order block reduction -> one partial row per chain
+  double* red = lds;
+  double* out = A.partial + ((size_t)shard * A.Gs + chunk) * C * A.PW;
+#pragma unroll
+  for (int m = 0; m < JPT; ++m)
+#pragma unroll
+    for (int c = 0; c < C; ++c) red[((w * C + c) * JPT + m) * 64 + lane] = gacc[m][c];
+  __syncthreads();
+  for (int i = tid; i < C * d; i += NT) {
+    const int c = i / d, j = i % d, m = j >> 6, l = j & 63;
+    const double v = ((red[((0 * C + c) * JPT + m) * 64 + l] + red[((1 * C + c) * JPT + m) * 64 + l]) +
+                      red[((2 * C + c) * JPT + m) * 64 + l]) + red[((3 * C + c) * JPT + m) * 64 + l];
+    out[(size_t)c * A.PW + 1 + j] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < CP; ++i) {
+    red[(size_t)(2 * i) * NT + tid] = lpa[i];
+    red[(size_t)(2 * i + 1) * NT + tid] = ga[i];
+  }
+  __syncthreads();
+  if (tid < 2 * C) {          // chain c's pairs: slot i = (c*64)/NT, threads (c*64)%NT .. +63
+    const int c = tid >> 1, kind = tid & 1;
+    const int i = (c * 64) / NT, t0 = (c * 64) % NT;
+    const double* src = red + (size_t)(2 * i + kind) * NT + t0;
+    double v = 0.0;
+    for (int k = 0; k < 64; ++k) v += src[k];
+    out[(size_t)c * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
+}
+
 // Sum chunk partials in chunk order and finish the family's lp / gradient.
 // grid (nshards*C, ceil(PW/64)), 256 threads: 4 waves split the chunks, fixed combine order.
 template <int FAM>
@@ -269,18 +460,36 @@ __global__ __launch_bounds__(256) void k_sweep_reduce(SweepArgs A, double* lp_ou
 using namespace stk;
 
 // Host-side geometry: depends only on (n, d) so reductions are identical on 1 or N GPUs.
+// v2 (d <= 128, even d) unless STARK_SWEEP=1 forces v1.
+static int sweep_variant(int d) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("STARK_SWEEP");
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced == 1) return 1;
+  return (d <= 128 && d % 2 == 0) ? 2 : 1;
+}
+
 void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_bytes, int C) {
   int t = 64;
   while (t > 8 && (int64_t)t * d > 8192) t >>= 1;
-  const int m = (256 / t) % 32;   // LD = m (mod 32): conflict-free ds_read_b64 in the forward pass
-  int ld = d;
-  while ((ld % 32) != m) ++ld;
   int64_t g = (n + (int64_t)8 * t - 1) / ((int64_t)8 * t);
   if (g > 512) g = 512;
   if (g < 1) g = 1;
   *T = t;
-  *LD = ld;
   *G = (int)g;
+  if (sweep_variant(d) == 2) {
+    *LD = d | 1;
+    const size_t main = (size_t)(64 * (d | 1) + 4 * C * 64 + 64 * C) * sizeof(double);
+    const size_t red = (size_t)std::max(4 * C * 2 * 64, 4 * 256) * sizeof(double);
+    *lds_bytes = std::max(main, red);
+    return;
+  }
+  const int m = (256 / t) % 32;   // LD = m (mod 32): conflict-free ds_read_b64 in the forward pass
+  int ld = d;
+  while ((ld % 32) != m) ++ld;
+  *LD = ld;
   const int JW = d <= 64 ? 64 : (d <= 128 ? 128 : 256);
   const int JPT = (d + JW - 1) / JW;
   const size_t main = (size_t)(t * ld + C * ld + t * C + 2 * C) * sizeof(double);
@@ -311,6 +520,15 @@ static hipError_t pick_vec(const SweepArgs& A, int d, int nblocks, size_t lds, h
 
 template <int FAM, int C>
 static hipError_t pick_tile(const SweepArgs& A, int d, int T, int nblocks, size_t lds, hipStream_t st) {
+  if (sweep_variant(d) == 2) {
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)k_sweep2<FAM, C>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL((k_sweep2<FAM, C>), dim3(nblocks), dim3(256), lds, st, A);
+    return hipGetLastError();
+  }
   switch (T) {
     case 64: return pick_vec<FAM, C, 64, 1>(A, d, nblocks, lds, st);
     case 32: return pick_vec<FAM, C, 32, 1>(A, d, nblocks, lds, st);

@@ -6,7 +6,9 @@ shards generated in HBM.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -16,6 +18,23 @@ from ._lib import (N_STATS, STAT_NAMES, STK_LINREG, STK_LOGREG, STK_SCHOOLS, Con
                    StarkHipError, check)
 
 FAMILIES = {"schools": STK_SCHOOLS, "linear": STK_LINREG, "logistic": STK_LOGREG}
+
+# Live library handles, closed in dependency order (samplers, models, contexts) before the
+# HIP runtime's own exit handlers run; after that every close() is a no-op.
+_live = {"sampler": weakref.WeakSet(), "model": weakref.WeakSet(), "ctx": weakref.WeakSet()}
+_finalized = False
+
+
+@atexit.register
+def _shutdown():
+    global _finalized
+    for kind in ("sampler", "model", "ctx"):
+        for obj in list(_live[kind]):
+            try:
+                obj.close()
+            except Exception:
+                pass
+    _finalized = True
 FAMILY_NAMES = {v: k for k, v in FAMILIES.items()}
 
 
@@ -43,6 +62,7 @@ class Context:
         check(lib.stk_ctx_create(int(device), ctypes.byref(h)))
         self._h = h
         self.device = device
+        _live["ctx"].add(self)
         if profiling:
             self.set_profiling(True)
 
@@ -57,9 +77,9 @@ class Context:
         return _lib.load().stk_ctx_stream(self._h) or 0
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and not _finalized:
             _lib.load().stk_ctx_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -93,7 +113,8 @@ class SampleResult:
 def make_config(num_warmup=1000, num_samples=1000, chains=1, max_depth=10, adapt_delta=0.8, adapt_gamma=0.05,
                 adapt_kappa=0.75, adapt_t0=10.0, stepsize=1.0, init_radius=2.0, adapt_init_buffer=75,
                 adapt_term_buffer=50, adapt_window=25, adapt_engaged=True, seed=1234, init=None,
-                inv_metric=None, skip_init_stepsize=False, iter_offset=0, shard_ids=None):
+                inv_metric=None, skip_init_stepsize=False, iter_offset=0, shard_ids=None,
+                save_warmup=False):
     """Stan sampler settings (pystan 2 `sampling()` keywords + control block)."""
     c = _lib.default_config()
     c.num_warmup, c.num_samples, c.chains, c.max_depth = int(num_warmup), int(num_samples), int(chains), int(max_depth)
@@ -116,6 +137,7 @@ def make_config(num_warmup=1000, num_samples=1000, chains=1, max_depth=10, adapt
         keep.append(shard_ids)
         c.shard_ids = shard_ids.ctypes.data
     c.skip_init_stepsize = int(bool(skip_init_stepsize))
+    c.save_warmup = int(bool(save_warmup))
     c.iter_offset = int(iter_offset)
     c._keep = keep   # keep buffers alive with the struct
     return c
@@ -131,6 +153,7 @@ class Model:
             self._h = _handle
         else:
             self._h = self._create(shards)
+        _live["model"].add(self)
         lib = _lib.load()
         self.nshards = len(shards) if shards is not None else self._nshards
         self.D, self.P, self.n_rows = [], [], []
@@ -250,9 +273,9 @@ class Model:
         return q, lp, st
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and not _finalized:
             _lib.load().stk_model_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -271,6 +294,7 @@ class Sampler:
         check(_lib.load().stk_sampler_create(model._h, ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
         self.total = cfg.num_warmup + cfg.num_samples
+        _live["sampler"].add(self)
 
     def run(self, target_iter: int | None = None, max_steps: int = 0):
         """Advance every chain to `target_iter` completed transitions (default: all)."""
@@ -291,7 +315,8 @@ class Sampler:
         return out, st
 
     def unconstrained(self, shard: int):
-        out = np.empty((self.cfg.chains, self.cfg.num_samples, self.model.D[shard]))
+        n = self.cfg.num_samples + (self.cfg.num_warmup if self.cfg.save_warmup else 0)
+        out = np.empty((self.cfg.chains, n, self.model.D[shard]))
         check(_lib.load().stk_sampler_draws_unconstrained(self._h, shard, out.ctypes.data))
         return out
 
@@ -314,9 +339,9 @@ class Sampler:
         return SampleResult(draws, stats, info, self.cfg.chains, self.cfg.num_samples)
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and not _finalized:
             _lib.load().stk_sampler_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
