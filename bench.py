@@ -4,13 +4,19 @@ fp64, 8 subposterior shards + consensus combine (BASELINE.json configs[3], the c
 metric is quoted on; 80 GB of X fits one MI355X, so N=1 runs all 8 shards on one GPU and
 N GPUs run 8/N shards each -- total work fixed, "scaling": "strong").
 
-A "step" = one NUTS transition of every chain on every shard (each transition is
-2^depth - 1 leapfrogs, i.e. that many fused data sweeps over the shard).  Timeline:
-  data generated in HBM (Philox, not timed) -> --adapt-iters warmup transitions with Stan's
-  adaptation (not timed) -> W untimed steps -> barrier+sync -> K timed steps -> sync+barrier.
-`value` = chain-gradient evaluations of all ranks in the timed region / max-over-ranks time.
-ESS/s = min over non-lp__ parameters of the ESS of the consensus-combined timed draws
-(all-gathered over RCCL, combined on the GPU) / the same time.
+A "step" = one pass of the hot path over the data: ONE fused log-density+gradient sweep of
+every local shard, i.e. one leapfrog of every chain (chains share a shard's sweep), followed
+by the deterministic chunk reduction and one NUTS state-machine step.  Chains are never held
+back by each other: each runs its own trajectories, transitions and draws.  Timeline:
+  data generated in HBM (Philox, not timed) -> Stan warmup with adaptation, --adapt-iters
+  transitions per chain (not timed) -> W untimed steps -> barrier+sync -> K timed steps ->
+  sync+barrier.
+`value` = chain-gradient evaluations of all ranks in the timed region / max-over-ranks time
+(every chain evaluates one gradient per step, so = chains * K / time).
+ESS/s: every chain contributes the M transitions it completed inside the timed window
+(M = the minimum over chains, so shards align); the consensus combine of those draws runs on
+the GPU after one all-gather; ESS/s = min over non-lp__ parameters of the combined draws'
+ESS / the timed window.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
 """
@@ -31,13 +37,13 @@ HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameter
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=100)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=1500)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--rows", type=float, default=1e8, help="total rows N over all shards")
     p.add_argument("--d", type=int, default=100)
     p.add_argument("--shards", type=int, default=8)
     p.add_argument("--chains", type=int, default=4, help="chains per shard (share one data sweep)")
-    p.add_argument("--adapt-iters", type=int, default=150)
+    p.add_argument("--adapt-iters", type=int, default=300)
     p.add_argument("--seed", type=int, default=20240)
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -109,8 +115,10 @@ def main():
     t_gen = time.perf_counter() - t
 
     A, W, K = a.adapt_iters, a.warmup, a.steps
-    sampler = model.sampler(num_warmup=A, num_samples=W + K, chains=a.chains, seed=a.seed + 1,
+    total = A + W + K + 1          # enough sampling iterations that no chain finishes in the window
+    sampler = model.sampler(num_warmup=A, num_samples=total - A, chains=a.chains, seed=a.seed + 1,
                             shard_ids=shard_ids)
+
     def log(msg):
         if rank == 0:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
@@ -124,7 +132,7 @@ def main():
         log(f"adaptation {min(it, A)}/{A}: {time.perf_counter() - t:.1f}s, leapfrogs/chain "
             f"{inf['leapfrogs'] / max(1, spr * a.chains):.0f}")
     t_adapt = time.perf_counter() - t
-    sampler.run(A + W)
+    sampler.run(total, max_steps=W)
     log(f"warmup steps done; timing {K} steps")
 
     def barrier():
@@ -132,22 +140,28 @@ def main():
         if dist:
             dist.barrier()
 
+    nchains = spr * a.chains
+    it0 = sampler.iterations()
     ctx.set_profiling(True)
     i0 = sampler.info()
     barrier()
     t0 = time.perf_counter()
-    sampler.run(A + W + K)
+    sampler.run(total, max_steps=K)
     ctx.sync()
     barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_profiling(False)
     i1 = sampler.info()
+    it1 = sampler.iterations()
 
     grads = i1["grad_evals"] - i0["grad_evals"]
     leaps = i1["leapfrogs"] - i0["leapfrogs"]
     sweeps = i1["sweeps"] - i0["sweeps"]
     shard_sweeps = i1["shard_sweeps"] - i0["shard_sweeps"]
     sweep_ms = i1["sweep_ms"] - i0["sweep_ms"]
+    done_in_window = it1 - it0                       # transitions completed per chain
+    m_local = int(done_in_window.min())
+    eps, _ = sampler.adaptation()
     if dist:
         v = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
@@ -155,17 +169,24 @@ def main():
         g = torch.tensor([grads, leaps], dtype=torch.float64, device="cuda")
         dist.all_reduce(g, op=dist.ReduceOp.SUM)
         grads, leaps = int(g[0].item()), int(g[1].item())
+        mm = torch.tensor([m_local], dtype=torch.int64, device="cuda")
+        dist.all_reduce(mm, op=dist.ReduceOp.MIN)
+        M = int(mm.item())
+    else:
+        M = m_local
 
-    # ---- timed draws -> consensus combine -> ESS
+    # ---- draws completed inside the window (first M per chain) -> consensus -> ESS
     P = model.P[0]
     local = {}
     for s in range(spr):
         dr, _ = sampler.draws(s)
-        cols = np.concatenate([np.arange(c * (W + K) + W, c * (W + K) + W + K) for c in range(a.chains)])
-        local[shard_ids[s]] = np.ascontiguousarray(dr[:, cols])
-    from stark_amd import dist as sdist
+        per = total - A
+        cols = []
+        for c in range(a.chains):
+            first = it0[s * a.chains + c] - A       # sampling index of the first window transition
+            cols.append(np.arange(c * per + first, c * per + first + M))
+        local[shard_ids[s]] = np.ascontiguousarray(dr[:, np.concatenate(cols)]) if M > 0 else None
     if dist:
-        # contiguous shard blocks per rank -> gather in global shard order
         allp = [None] * a.shards
         gathered = [None] * world
         dist.all_gather_object(gathered, local)
@@ -175,9 +196,9 @@ def main():
     else:
         allp = [local[k_] for k_ in range(a.shards)]
     ess_ps, min_ess, sub_ess = None, None, None
-    if rank == 0:
+    if rank == 0 and M >= 4:
         sub_ess = float(np.nanmin(diagnostics.ess_matrix(allp[0][:-1], a.chains)))
-        if a.chains * K > P + 1:
+        if a.chains * M > P + 1:
             comb, used = engine.consensus(allp, ctx)
             e = diagnostics.ess_matrix(comb[:-1], a.chains)     # drop lp__
             min_ess = float(np.nanmin(e))
@@ -201,8 +222,10 @@ def main():
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            if tj.get("rows_per_shard") == rows_per_shard and tj.get("d") == a.d and tj.get("shards_per_gpu") == spr:
-                traffic = tj.get("hbm_bytes_per_launch")
+            if tj.get("rows_per_shard") == rows_per_shard and tj.get("d") == a.d and tj.get("hbm_bytes_per_shard_sweep"):
+                # PMC pass of the same shard geometry (tools/pmc_traffic.py): FETCH_SIZE x2 per
+                # shard sweep, times the shards a launch swept on average
+                traffic = tj["hbm_bytes_per_shard_sweep"] * shard_sweeps / max(sweeps, 1)
         except Exception:
             traffic = None
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -232,7 +255,10 @@ def main():
         "ess_per_sec": ess_ps,
         "min_ess": min_ess,
         "subposterior_min_ess_shard0": sub_ess,
-        "leapfrogs_per_transition": leaps / max(1, a.shards * a.chains * K),
+        "transitions_per_chain_in_window": {"min": int(done_in_window.min()), "median": float(np.median(done_in_window)),
+                                            "max": int(done_in_window.max()), "used_for_ess": M},
+        "stepsize_per_chain": {"min": float(eps.min()), "median": float(np.median(eps)), "max": float(eps.max())},
+        "leapfrogs_per_transition": float(nchains * K / max(1, done_in_window.sum())),
         "rows_x_chains_per_sec": grads * rows_per_shard / elapsed,
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -152,6 +152,8 @@ STK_API int stk_sampler_draws(stk_sampler* s, int shard, double* out, double* st
  * out[chains][num_warmup + num_samples][D] when cfg.save_warmup is set. */
 STK_API int stk_sampler_draws_unconstrained(stk_sampler* s, int shard, double* out);
 STK_API int stk_sampler_adaptation(stk_sampler* s, double* stepsize, double* inv_metric);
+/* Transitions completed so far by every chain (nshards * chains, shard-major). */
+STK_API int stk_sampler_iterations(stk_sampler* s, int32_t* iters);
 STK_API int stk_sampler_destroy(stk_sampler* s);
 STK_API int stk_sample(stk_model* m, const stk_config* cfg, double* draws, double* stats, stk_run_info* info);
 

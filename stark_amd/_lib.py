@@ -87,6 +87,7 @@ SIGNATURES = [
     ("stk_sampler_draws", ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp]),
     ("stk_sampler_draws_unconstrained", ctypes.c_int, [_vp, ctypes.c_int, _vp]),
     ("stk_sampler_adaptation", ctypes.c_int, [_vp, _vp, _vp]),
+    ("stk_sampler_iterations", ctypes.c_int, [_vp, _vp]),
     ("stk_sampler_destroy", ctypes.c_int, [_vp]),
     ("stk_sample", ctypes.c_int, [_vp, ctypes.POINTER(Config), _vp, _vp, ctypes.POINTER(RunInfo)]),
     ("stk_transition", ctypes.c_int, [_vp, ctypes.c_int, _vp, _i32, _u64, _i32, _dbl, _vp, _i32, _vp, _vp]),

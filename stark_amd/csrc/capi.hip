@@ -806,6 +806,16 @@ int stk_sampler_adaptation(stk_sampler* s, double* stepsize, double* inv_metric)
   return STK_OK;
 }
 
+int stk_sampler_iterations(stk_sampler* s, int32_t* iters) {
+  ARG_CHECK(s && iters, "stk_sampler_iterations: bad arguments");
+  stk_ctx* ctx = s->m->ctx;
+  STK_HIP_CHECK(hipSetDevice(ctx->device));
+  STK_HIP_CHECK(hipMemcpy2DAsync(iters, sizeof(int32_t), s->A.iv + I_ITER, sizeof(int) * I_COUNT, sizeof(int32_t),
+                                 s->A.nchains, hipMemcpyDefault, ctx->stream));
+  STK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  return STK_OK;
+}
+
 int stk_sample(stk_model* m, const stk_config* cfg, double* draws, double* stats, stk_run_info* info) {
   stk_sampler* s = nullptr;
   RC(stk_sampler_create(m, cfg, &s));

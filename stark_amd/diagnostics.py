@@ -57,6 +57,8 @@ def ess(chains) -> float:
             rho[t + 1] = (rho[t - 1] + rho[t]) / 2.0
             rho[t + 2] = rho[t + 1]
     tau = -1.0 + 2.0 * rho[:max_s].sum() + rho[max_s + 1]
+    # guard for very short / antithetic chains, as later Stan releases do
+    tau = max(tau, 1.0 / np.log10(nc * n))
     return float(nc * n / tau)
 
 

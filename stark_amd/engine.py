@@ -320,6 +320,13 @@ class Sampler:
         check(_lib.load().stk_sampler_draws_unconstrained(self._h, shard, out.ctypes.data))
         return out
 
+    def iterations(self) -> np.ndarray:
+        """Transitions completed by every chain (shard-major), warmup included."""
+        n = self.model.nshards * self.cfg.chains
+        out = np.empty(n, np.int32)
+        check(_lib.load().stk_sampler_iterations(self._h, out.ctypes.data))
+        return out
+
     def adaptation(self):
         n = self.model.nshards * self.cfg.chains
         eps = np.empty(n)
