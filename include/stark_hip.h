@@ -95,6 +95,8 @@ typedef struct {
   const int32_t* shard_ids;  /* NULL, or the GLOBAL index of every local shard: chain c of shard s
                                 draws from RNG stream shard_ids[s] * chains + c, so a shard samples
                                 identically whichever GPU (and with whichever other shards) it runs */
+  double stepsize_jitter;    /* Stan control stepsize_jitter in [0, 1]: every transition uses
+                                stepsize * (1 + jitter * U(-1, 1)) (base_hmc::sample_stepsize) */
 } stk_config;
 
 typedef struct {

@@ -28,7 +28,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
 
 FAM_SCHOOLS, FAM_LINREG, FAM_LOGREG = 1, 2, 3
-TAG_INIT, TAG_MOM, TAG_UNI, TAG_SSMOM, TAG_X, TAG_Y, TAG_BETA = 0x1, 0x2, 0x3, 0x4, 0x10, 0x11, 0x12
+TAG_INIT, TAG_MOM, TAG_UNI, TAG_SSMOM, TAG_JIT, TAG_X, TAG_Y, TAG_BETA = 0x1, 0x2, 0x3, 0x4, 0x5, 0x10, 0x11, 0x12
 
 
 def build() -> str:
@@ -133,7 +133,7 @@ class _Cfg(ctypes.Structure):
                 ("adapt_delta", ctypes.c_double), ("gamma", ctypes.c_double), ("kappa", ctypes.c_double),
                 ("t0", ctypes.c_double), ("stepsize", ctypes.c_double), ("init_radius", ctypes.c_double),
                 ("init_buffer", ctypes.c_int), ("term_buffer", ctypes.c_int), ("window", ctypes.c_int),
-                ("adapt_engaged", ctypes.c_int), ("seed", ctypes.c_uint64)]
+                ("adapt_engaged", ctypes.c_int), ("seed", ctypes.c_uint64), ("stepsize_jitter", ctypes.c_double)]
 
 
 class Model:
@@ -178,9 +178,9 @@ class Model:
     def run_chain(self, *, num_warmup=1000, num_samples=1000, max_depth=10, adapt_delta=0.8,
                   gamma=0.05, kappa=0.75, t0=10.0, stepsize=1.0, init_radius=2.0,
                   init_buffer=75, term_buffer=50, window=25, adapt_engaged=True, seed=1234,
-                  gid=0, init=None):
+                  gid=0, init=None, stepsize_jitter=0.0):
         cfg = _Cfg(num_warmup, num_samples, max_depth, adapt_delta, gamma, kappa, t0, stepsize,
-                   init_radius, init_buffer, term_buffer, window, int(adapt_engaged), seed)
+                   init_radius, init_buffer, term_buffer, window, int(adapt_engaged), seed, stepsize_jitter)
         T = num_warmup + num_samples
         q = np.empty((T, self.D))
         lp = np.empty(T)

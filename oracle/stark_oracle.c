@@ -60,7 +60,7 @@ void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint3
 }
 
 /* Stream tags (counter word 3).  Same values as stark_amd/csrc/philox.h. */
-enum { TAG_INIT = 0x1, TAG_MOM = 0x2, TAG_UNI = 0x3, TAG_SSMOM = 0x4,
+enum { TAG_INIT = 0x1, TAG_MOM = 0x2, TAG_UNI = 0x3, TAG_SSMOM = 0x4, TAG_JIT = 0x5,
        TAG_X = 0x10, TAG_Y = 0x11, TAG_BETA = 0x12 };
 
 static void philox_u64x2(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
@@ -267,13 +267,14 @@ typedef struct {
   double adapt_delta, gamma, kappa, t0, stepsize, init_radius;
   int init_buffer, term_buffer, window, adapt_engaged;
   uint64_t seed;
+  double stepsize_jitter;
 } orc_cfg;
 
 typedef struct {
   const orc_data* m;
   int D;
   double* inv_metric;
-  double eps, nom_eps;
+  double eps, nom_eps, jitter;
   int max_depth;
   double max_deltaH;
   uint64_t seed;
@@ -390,7 +391,9 @@ typedef struct { double accept, eps, depth, n_leapfrog, divergent, energy; } orc
 /* base_nuts::transition (Stan 2.19.1).  s->z holds the start point with V and g valid. */
 static void transition(nuts* s, orc_stats* st) {
   int D = s->D;
-  s->eps = s->nom_eps;          /* sample_stepsize with jitter 0 */
+  s->eps = s->nom_eps;          /* base_hmc::sample_stepsize */
+  if (s->jitter > 0)            /* own stream (TAG_JIT): the TAG_UNI indices do not move */
+    s->eps *= 1.0 + s->jitter * (2.0 * orc_uniform(s->seed, s->gid, s->iter, 0, TAG_JIT) - 1.0);
   s->uk = 0;
   sample_p(s, &s->z, s->iter, 0, TAG_MOM);
   ps_point z_plus, z_minus, z_sample, z_propose;
@@ -571,6 +574,7 @@ long orc_run_chain(const orc_data* m, const orc_cfg* cfg, uint32_t gid, const do
     s.z.q[i] = init ? init[i] : -cfg->init_radius + 2.0 * cfg->init_radius * orc_uniform(cfg->seed, gid, 0, (uint32_t)i, TAG_INIT);
   update_potential_gradient(&s, &s.z);
   s.nom_eps = cfg->stepsize;
+  s.jitter = cfg->stepsize_jitter;
   s.delta = cfg->adapt_delta; s.gamma = cfg->gamma; s.kappa = cfg->kappa; s.t0 = cfg->t0;
   s.mu = log(10.0 * cfg->stepsize);
   da_restart(&s);

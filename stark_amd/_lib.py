@@ -46,7 +46,8 @@ class Config(ctypes.Structure):
                 ("adapt_window", ctypes.c_int32), ("adapt_engaged", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("init", ctypes.c_void_p), ("inv_metric", ctypes.c_void_p),
                 ("skip_init_stepsize", ctypes.c_int32), ("iter_offset", ctypes.c_int32),
-                ("save_warmup", ctypes.c_int32), ("shard_ids", ctypes.c_void_p)]
+                ("save_warmup", ctypes.c_int32), ("shard_ids", ctypes.c_void_p),
+                ("stepsize_jitter", ctypes.c_double)]
 
 
 class RunInfo(ctypes.Structure):

@@ -22,7 +22,7 @@ hipError_t stk_launch_schools_lpgrad(const ShardDev* shards, int shard, int nch,
                                      double* lp, double* g, hipStream_t st);
 void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_bytes, int C);
 bool stk_sweep_supported(int C, int d);
-hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, int nsh, int d, int T, int LD, int G,
+hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, int nsh, int64_t n, int d, int T, int LD, int G,
                             int Gs, size_t lds, const double* q, int C, int Dp, double* partial, const int* req_step,
                             int step_id, int* ran, hipStream_t st);
 hipError_t stk_launch_sweep_reduce(int family, const ShardDev* shards_dev, int shard0, int nsh, int d, int G, int Gs,
@@ -422,7 +422,7 @@ int stk_log_density_grad(stk_model* m, int shard, const double* q, int32_t C, do
   } else {
     int T, LD, G;
     size_t lds;
-    const int Cb = 8;
+    const int Cb = C <= 1 ? 1 : (C <= 2 ? 2 : 4);   // the chain batch the sampler's sweep uses
     stk_sweep_geometry(s.n, s.d, &T, &LD, &G, &lds, Cb);
     const int PW = s.d + 2;
     RC(ctx->scratch[0].ensure(sizeof(double) * (size_t)(m->nshards * Cb) * Dp));
@@ -437,7 +437,7 @@ int stk_log_density_grad(stk_model* m, int shard, const double* q, int32_t C, do
         const int src = c0 + std::min(c, nb - 1);
         STK_HIP_CHECK(hipMemcpyAsync(qb + (size_t)c * Dp, q + (size_t)src * D, sizeof(double) * D, hipMemcpyDefault, st));
       }
-      STK_HIP_CHECK(stk_launch_sweep(m->family, shd, shard, 1, s.d, T, LD, G, G, lds, ctx->scratch[0].as<double>(), Cb,
+      STK_HIP_CHECK(stk_launch_sweep(m->family, shd, shard, 1, s.n, s.d, T, LD, G, G, lds, ctx->scratch[0].as<double>(), Cb,
                                      Dp, ctx->scratch[3].as<double>(), nullptr, 0, nullptr, st));
       STK_HIP_CHECK(stk_launch_sweep_reduce(m->family, shd, shard, 1, s.d, G, G, ctx->scratch[0].as<double>(), Cb, Dp,
                                             ctx->scratch[3].as<double>(), nullptr, 0, ctx->scratch[1].as<double>(),
@@ -490,6 +490,7 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   ARG_CHECK(cfg->max_depth >= 1 && cfg->max_depth <= 30, "max_depth must be in [1, 30]");
   ARG_CHECK(cfg->adapt_delta > 0 && cfg->adapt_delta < 1, "adapt_delta must be in (0, 1)");
   ARG_CHECK(cfg->stepsize > 0, "stepsize must be positive");
+  ARG_CHECK(cfg->stepsize_jitter >= 0 && cfg->stepsize_jitter <= 1, "stepsize_jitter must be in [0, 1]");
   stk_ctx* ctx = m->ctx;
   STK_HIP_CHECK(hipSetDevice(ctx->device));
   const int nch = stk_nch_for(m->Dmax);
@@ -530,6 +531,7 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   A.kappa = cfg->adapt_kappa;
   A.t0 = cfg->adapt_t0;
   A.seed = cfg->seed;
+  A.jitter = cfg->stepsize_jitter;
   A.S_total = cfg->chains * cfg->num_samples;
   A.Pmax = m->Pmax;
   A.shards = m->sh_dev.as<ShardDev>();
@@ -672,7 +674,7 @@ static int run_split_batch(stk_sampler* s, int nsteps, int pause_at) {
     const int step_id = s->step;
     if (prof) STK_HIP_CHECK(hipEventRecord(s->ev[2 * k], st));
     for (const auto& gr : s->groups) {
-      STK_HIP_CHECK(stk_launch_sweep(m->family, A.shards, gr.shard0, gr.nsh, m->d, gr.T, gr.LD, gr.G, s->Gs, gr.lds,
+      STK_HIP_CHECK(stk_launch_sweep(m->family, A.shards, gr.shard0, gr.nsh, m->sh[gr.shard0].n, m->d, gr.T, gr.LD, gr.G, s->Gs, gr.lds,
                                      A.qeval, A.C, A.Dp, s->partial.as<double>(), A.req_step, step_id,
                                      prof ? s->ran.as<int>() : nullptr, st));
     }

@@ -89,6 +89,7 @@ struct NutsArgs {
   int ud_iters;     // transitions stored per chain
   int* req_step;    // nshards: last step index that issued a request for the shard
   const int* shard_ids;  // nullptr or global shard index per local shard (RNG stream keys)
+  double jitter;         // stepsize_jitter (0: off)
 };
 
 // RNG stream of a chain: global shard index * chains + chain.

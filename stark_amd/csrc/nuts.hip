@@ -303,7 +303,9 @@ struct NutsChain {
 
   __device__ void start_transition() {
     iv[I_MODE] = M_TRAJ;
-    s[S_EPS] = s[S_NOMEPS];
+    s[S_EPS] = s[S_NOMEPS];   // base_hmc::sample_stepsize; jitter on its own stream (TAG_JIT)
+    if (A.jitter > 0)
+      s[S_EPS] *= 1.0 + A.jitter * (2.0 * uniform_at(A.seed, rid, (uint32_t)(iv[I_ITER] + A.iter_offset), 0u, TAG_JIT) - 1.0);
     iv[I_UK] = 0;
     load_sample_point();
     sample_momentum((uint32_t)(iv[I_ITER] + A.iter_offset), 0u, TAG_MOM);

@@ -6,6 +6,7 @@
 //   TAG_MOM   ctr = {chain_gid, iteration, i/2,               TAG}  momentum (Box-Muller)
 //   TAG_UNI   ctr = {chain_gid, iteration, k/2,               TAG}  k-th uniform of a transition
 //   TAG_SSMOM ctr = {chain_gid, ss_call,   probe<<12 | i/2,   TAG}  init_stepsize momenta
+//   TAG_JIT   ctr = {chain_gid, iteration, 0,                 TAG}  stepsize jitter of a transition
 //   TAG_X     ctr = {row_lo, row_hi,       j/2,               TAG}  synthetic X_ij
 //   TAG_Y     ctr = {row_lo, row_hi,       0,                 TAG}  synthetic y_i noise
 //   TAG_BETA  ctr = {j/2, 0, 0, TAG}                                 synthetic beta_j
@@ -17,7 +18,7 @@
 
 namespace stk {
 
-enum : uint32_t { TAG_INIT = 0x1, TAG_MOM = 0x2, TAG_UNI = 0x3, TAG_SSMOM = 0x4,
+enum : uint32_t { TAG_INIT = 0x1, TAG_MOM = 0x2, TAG_UNI = 0x3, TAG_SSMOM = 0x4, TAG_JIT = 0x5,
                   TAG_X = 0x10, TAG_Y = 0x11, TAG_BETA = 0x12 };
 
 struct u64x2 { uint64_t a, b; };

@@ -408,6 +408,268 @@ __global__ __launch_bounds__(256, 2) void k_sweep2(SweepArgs A) {
   }
 }
 
+// v3 sweep (even d <= 104, C <= 4): wave-private LDS-DMA rings, no barrier in the main loop.
+//
+// v2 holds one tile ahead in registers per block; with two blocks per CU that leaves too few
+// bytes in flight (tools/sweep_micro.hip: the v2 pipeline without arithmetic reaches only
+// 3.7-4.5 TB/s against 6.1 TB/s for a plain streaming read).  Here one 512-thread block per
+// CU streams a chunk of 64-row tiles; wave w owns rows [8w, 8w+8) of every tile and moves
+// them itself: `buffer_load_dwordx4 ... lds` (1 KiB per wave-instruction, no VGPR staging,
+// no ds_write pass) into a private ring of NB 8-row slots, so while it computes sub-tile t
+// its sub-tiles t+1 .. t+NB-1 are in flight (8 waves x 2 x 6.4 KB at d = 100) and it never
+// waits for another wave: counted vmcnt on its own DMAs only, no s_barrier until the final
+// reduction (a block-wide barrier per tile put all waves in lockstep and exposed the whole
+// forward -> residual -> backward latency chain every tile).  Per sub-tile:
+//   forward   8 lanes per row, lane i reads 16-B pieces i, i+8, ... of its row (ds_read_b128)
+//             and keeps its beta pieces in registers for the whole launch; 3 xor steps sum
+//             the row;
+//   residual  lane i < C of each row group finishes chain i (Stan's bernoulli_logit cutoffs /
+//             normal residual), d eta -> a per-wave LDS scratch;
+//   backward  lane k = piece k (2 columns), 8 rows, d eta read as broadcasts.
+// Chunks are whole tiles ([64*t0, 64*t1) rows, a function of (n, d) only) and all sums run in
+// a fixed order, so the result is bitwise independent of shard placement, as for v1/v2.
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  // s_waitcnt encoding (gfx9): vmcnt [3:0] + [15:14], expcnt [6:4] = 7, lgkmcnt [11:8] = 15
+#define STK_VMCNT(N) case N: __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0xF70); break;
+  switch (n) {
+    STK_VMCNT(0) STK_VMCNT(1) STK_VMCNT(2) STK_VMCNT(3) STK_VMCNT(4) STK_VMCNT(5) STK_VMCNT(6)
+    STK_VMCNT(7) STK_VMCNT(8) STK_VMCNT(9) STK_VMCNT(10) STK_VMCNT(11) STK_VMCNT(12) STK_VMCNT(13)
+    STK_VMCNT(14) STK_VMCNT(15) STK_VMCNT(16) STK_VMCNT(17) STK_VMCNT(18) STK_VMCNT(19) STK_VMCNT(20)
+    STK_VMCNT(21) STK_VMCNT(22) STK_VMCNT(23) STK_VMCNT(24) STK_VMCNT(25) STK_VMCNT(26) STK_VMCNT(27)
+    default: __builtin_amdgcn_s_waitcnt(0xF70); break;   // vmcnt(0)
+  }
+#undef STK_VMCNT
+}
+
+constexpr int S3_T = 64;          // rows per tile
+constexpr int S3_W = 8;           // waves per block
+constexpr int S3_MAXP = 7;        // pieces per lane in the forward: K <= 56
+constexpr int S3_KMAX = 52;       // pieces per row (d/2) handled by v3
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+// DPP lane exchange of a double (full-rate VALU, no LDS round trip like ds_bpermute).
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// Sum over each group of 8 consecutive lanes; every lane of the group gets the total:
+// xor 1, xor 2 (quad_perm), then row_half_mirror (lane i <-> 7 - i) joins the two quads.
+__device__ __forceinline__ double sum8(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  return v + dpp_d<0x141>(v);
+}
+
+// -log1p(exp(-x)) and its derivative weight exp(-x)/(1+exp(-x)) for |x| <= 20 (Stan's
+// bernoulli_logit middle branch) with one exp, one log and one reciprocal: with u = 1 + e,
+// log1p(e) = log(u) - ((u - 1) - e)/u (the rounding of u corrected to first order), and
+// e/(1+e) = e * (1/u); 1/u by v_rcp_f64 + two Newton steps.
+__device__ __forceinline__ void softplus_terms(double x, double* lp_term, double* w) {
+  const double e = exp(-x);
+  const double u = 1.0 + e;
+  double r = __builtin_amdgcn_rcp(u);
+  r = fma(r, fma(-u, r, 1.0), r);
+  r = fma(r, fma(-u, r, 1.0), r);
+  *lp_term = log(u) - ((u - 1.0) - e) * r;
+  *w = e * r;
+}
+
+// One wave's ring slot: 8 rows of X (8 * 16 * K bytes) + 8 rows of y (<= 64 B), 16-B aligned.
+__host__ __device__ constexpr int sweep3_slot_bytes(int K) { return 8 * 16 * K + 64; }
+
+// Buffer descriptor built from readfirstlane'd inputs, so the compiler can prove it
+// wave-uniform and keeps it in SGPRs (no waterfall loop around every buffer op).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int64_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
+}
+
+// ABL (micro-benchmark ablations only, tools/sweep_micro.hip; 0 in the product): bit 0 replaces
+// the residual's transcendentals by a linear stand-in, bit 1 skips the backward, bit 2 the forward.
+template <int FAM, int C, int ABL = 0>
+__global__ __launch_bounds__(512) void k_sweep3(SweepArgs A, int NB) {
+  constexpr int T = S3_T, NW = S3_W;
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d, K = d >> 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int64_t nt = (sh.n + T - 1) / T;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * T, r1 = std::min<int64_t>(sh.n, t1 * T);
+  const int ntiles = (int)(t1 - t0);
+  constexpr int YB = (FAM == STK_LOGREG) ? 4 : 8;   // y bytes per row
+  const int SB = 8 * 16 * K;                        // X bytes of one wave's 8-row sub-tile
+  const int SS = sweep3_slot_bytes(K);              // slot: X [0, SB), y [SB, SB + 8*YB)
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const ring = reinterpret_cast<char*>(lds) + (size_t)w * NB * SS;   // this wave's NB slots
+  double* const dsc = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * NB * SS);  // [NW][8][C]
+
+  // ---- per-lane constants: beta pieces (forward) and alpha / 1/sigma (residual)
+  const double* qs = A.q + (size_t)shard * C * A.Dp;
+  const int fi = lane & 7, frow = w * 8 + (lane >> 3);   // forward: lane-in-row, row in tile
+  double bt[S3_MAXP][C][2];
+#pragma unroll
+  for (int m = 0; m < S3_MAXP; ++m) {
+    const int k = fi + 8 * m;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      bt[m][c][0] = k < K ? qs[(size_t)c * A.Dp + 1 + 2 * k] : 0.0;
+      bt[m][c][1] = k < K ? qs[(size_t)c * A.Dp + 2 + 2 * k] : 0.0;
+    }
+  }
+  const int rc = fi < C ? fi : 0;                        // residual chain of this lane
+  const double alpha = qs[(size_t)rc * A.Dp];
+  const double inv_s = (FAM == STK_LINREG) ? exp(-qs[(size_t)rc * A.Dp + d + 1]) : 0.0;
+  __builtin_amdgcn_s_waitcnt(0xF70);                      // ordinary loads retired before the DMAs start
+
+  // ---- DMA issue: sub-tile t of this wave = rows [64 t + 8 w, 64 t + 8 w + 8) of the chunk:
+  // nx 1-KiB X pieces (the last one partial) + one size-4 piece for y; buffer descriptors cover
+  // exactly the chunk, so a partial last tile reads zeros past its end instead of faulting.
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (r1 - r0) * d * 8);
+  const void* ybase = (FAM == STK_LOGREG) ? (const void*)(sh.yi + r0) : (const void*)(sh.y + r0);
+  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(ybase, (r1 - r0) * YB);
+  const int nx = (SB + 1023) >> 10;
+  const int last_lanes = (SB - ((nx - 1) << 10)) >> 4;
+  const int per_tile = nx + 1;                            // DMAs this wave issues per sub-tile
+  auto issue = [&](int t) {
+    char* sl = ring + (size_t)(t % NB) * SS;
+    const int xoff = (t * 64 + w * 8) * 16 * K;
+    for (int j = 0; j < nx - 1; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(sl + j * 1024), 16, lane * 16, xoff + j * 1024, 0, 0);
+    if (lane < last_lanes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(sl + (nx - 1) * 1024), 16, lane * 16,
+                                               xoff + (nx - 1) * 1024, 0, 0);
+    if (lane < 2 * YB)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_vptr)(sl + SB), 4, lane * 4, (t * 64 + w * 8) * YB, 0, 0);
+  };
+
+  double gacc[C][2];
+  double lpa = 0.0, gaa = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) gacc[c][0] = gacc[c][1] = 0.0;
+
+  for (int t = 0; t < NB - 1 && t < ntiles; ++t) issue(t);
+  for (int t = 0; t < ntiles; ++t) {
+    // own DMAs of sub-tile t retired; later sub-tiles (issued already) stay in flight
+    const int later = std::min(NB - 2, ntiles - 1 - t);
+    wait_vmcnt(later * per_tile);
+    __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): reads of slot t-1 are done
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NB - 1 < ntiles) issue(t + NB - 1);          // into slot (t-1) % NB
+    const char* xs = ring + (size_t)(t % NB) * SS - (size_t)w * 8 * 16 * K;   // row r of the tile at r*16K
+    const char* ys = xs + (size_t)w * 8 * 16 * K + SB - (size_t)w * 8 * YB;   // y of row r at r*YB
+    const int rows = (int)std::min<int64_t>(T, r1 - r0 - (int64_t)t * T);
+
+    // ---- forward: eta partial of row frow over this lane's pieces, then the row sum
+    double acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = 0.0;
+#pragma unroll
+    for (int m = 0; m < ((ABL & 4) ? 0 : S3_MAXP); ++m) {
+      const int k = std::min(fi + 8 * m, K - 1);
+      const dbl2 x = *reinterpret_cast<const dbl2*>(xs + ((size_t)frow * K + k) * 16);
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] = fma(x.y, bt[m][c][1], fma(x.x, bt[m][c][0], acc[c]));
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = sum8(acc[c]);
+
+    // ---- residual: lane fi < C finishes chain fi of row frow
+    if (fi < C) {
+      double eta = acc[0];
+#pragma unroll
+      for (int c = 1; c < C; ++c)
+        if (fi == c) eta = acc[c];
+      eta += alpha;
+      double de = 0.0;
+      if (frow < rows) {
+        if constexpr (ABL & 1) {
+          const int32_t yv = *reinterpret_cast<const int32_t*>(ys + frow * 4);
+          de = (2.0 * yv - 1.0) - 0.25 * eta;
+          lpa -= de * de;
+        } else if constexpr (FAM == STK_LOGREG) {
+          const int32_t yv = *reinterpret_cast<const int32_t*>(ys + frow * 4);
+          const double sgn = 2.0 * yv - 1.0;
+          const double ntt = sgn * eta;
+          if (ntt > 20.0) { const double e = exp(-ntt); lpa -= e; de = sgn * e; }
+          else if (ntt < -20.0) { lpa += ntt; de = sgn; }
+          else { double lt, wt; softplus_terms(ntt, &lt, &wt); lpa -= lt; de = sgn * wt; }
+        } else {
+          const double yv = *reinterpret_cast<const double*>(ys + frow * 8);
+          const double z = (yv - eta) * inv_s;
+          lpa += z * z;
+          de = z * inv_s;
+        }
+        gaa += de;
+      }
+      dsc[(w * 8 + (lane >> 3)) * C + fi] = de;
+    }
+
+    // ---- backward: lane = piece k (columns 2k, 2k+1), the wave's 8 rows
+    {
+      const int k = std::min(lane, K - 1);
+      const int nr = (ABL & 2) ? 0 : std::min(8, rows - w * 8);
+      auto row = [&](int rr) {
+        const dbl2 x = *reinterpret_cast<const dbl2*>(xs + ((size_t)(w * 8 + rr) * K + k) * 16);
+        const double* dr = dsc + (w * 8 + rr) * C;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const double dv = dr[c];
+          gacc[c][0] = fma(x.x, dv, gacc[c][0]);
+          gacc[c][1] = fma(x.y, dv, gacc[c][1]);
+        }
+      };
+      if (nr == 8) {            // full sub-tile: branch-free, the compiler pipelines the reads
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) row(rr);
+      } else {
+        for (int rr = 0; rr < nr; ++rr) row(rr);
+      }
+    }
+  }
+
+  // ---- fixed-order block reduction -> one partial row per chain
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __syncthreads();
+  double* red = lds;                                    // [NW][C][64][2] then [NW][64][2]
+  if (lane < K) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      red[((size_t)(w * C + c) * 64 + lane) * 2 + 0] = gacc[c][0];
+      red[((size_t)(w * C + c) * 64 + lane) * 2 + 1] = gacc[c][1];
+    }
+  }
+  double* red2 = red + (size_t)NW * C * 128;
+  red2[(size_t)tid * 2 + 0] = lpa;
+  red2[(size_t)tid * 2 + 1] = gaa;
+  __syncthreads();
+  double* out = A.partial + ((size_t)shard * A.Gs + chunk) * C * A.PW;
+  for (int i = tid; i < C * d; i += NW * 64) {
+    const int c = i / d, j = i % d, k = j >> 1, h = j & 1;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww) v += red[((size_t)(ww * C + c) * 64 + k) * 2 + h];
+    out[(size_t)c * A.PW + 1 + j] = v;
+  }
+  if (tid < 2 * C) {          // chain c: lanes with lane % 8 == c of every wave, in (wave, lane) order
+    const int c = tid >> 1, kind = tid & 1;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww)
+      for (int g = 0; g < 8; ++g) v += red2[(size_t)(ww * 64 + g * 8 + c) * 2 + kind];
+    out[(size_t)c * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
+}
+
 // Sum chunk partials in chunk order and finish the family's lp / gradient.
 // grid (nshards*C, ceil(PW/64)), 256 threads: 4 waves split the chunks, fixed combine order.
 template <int FAM>
@@ -459,19 +721,54 @@ __global__ __launch_bounds__(256) void k_sweep_reduce(SweepArgs A, double* lp_ou
 
 using namespace stk;
 
-// Host-side geometry: depends only on (n, d) so reductions are identical on 1 or N GPUs.
-// v2 (d <= 128, even d) unless STARK_SWEEP=1 forces v1.
-static int sweep_variant(int d) {
+// Host-side geometry: depends only on (n, d, C) so reductions are identical on 1 or N GPUs.
+// v3 (LDS-DMA ring) for even d <= 104 and C <= 4, v2 for other even d <= 128, else v1;
+// STARK_SWEEP=1|2|3 forces a variant where it applies (micro-benchmarks, A/B tests).
+static int sweep_forced() {
   static int forced = -1;
   if (forced < 0) {
     const char* e = getenv("STARK_SWEEP");
     forced = e ? atoi(e) : 0;
   }
-  if (forced == 1) return 1;
-  return (d <= 128 && d % 2 == 0) ? 2 : 1;
+  return forced;
+}
+
+// Ring depth of v3: as many slots per wave as fit next to the d-eta scratch (at most 5).
+static int sweep3_nb(int d, int C) {
+  const size_t fixed = (size_t)S3_W * 8 * C * sizeof(double);
+  const size_t per = (size_t)S3_W * sweep3_slot_bytes(d / 2);
+  int nb = (int)((160 * 1024 - fixed) / per);
+  return std::min(nb, 5);
+}
+
+static int sweep_variant(int64_t n, int d, int C) {
+  const int f = sweep_forced();
+  const bool v3ok = d % 2 == 0 && d / 2 <= S3_KMAX && (C == 1 || C == 2 || C == 4) && sweep3_nb(d, C) >= 3 &&
+                    (n * d * 8) / 512 < ((int64_t)1 << 30);
+  const bool v2ok = d <= 128 && d % 2 == 0;
+  if (f == 1) return 1;
+  if (f == 2) return v2ok ? 2 : 1;
+  if (v3ok) return 3;
+  return v2ok ? 2 : 1;
 }
 
 void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_bytes, int C) {
+  const int var = sweep_variant(n, d, C);
+  if (var == 3) {
+    const int64_t nt = (n + S3_T - 1) / S3_T;
+    int64_t g = (nt + 7) / 8;            // >= 8 tiles per chunk
+    if (g > 512) g = 512;
+    if (g < 1) g = 1;
+    const int nb = sweep3_nb(d, C);
+    *T = S3_T;
+    *LD = nb;
+    *G = (int)g;
+    const int K = d / 2;
+    const size_t ring = (size_t)S3_W * nb * sweep3_slot_bytes(K) + (size_t)S3_W * 8 * C * sizeof(double);
+    const size_t red = ((size_t)S3_W * C * 128 + (size_t)S3_W * 64 * 2) * sizeof(double);
+    *lds_bytes = std::max(ring, red);
+    return;
+  }
   int t = 64;
   while (t > 8 && (int64_t)t * d > 8192) t >>= 1;
   int64_t g = (n + (int64_t)8 * t - 1) / ((int64_t)8 * t);
@@ -479,7 +776,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
   if (g < 1) g = 1;
   *T = t;
   *G = (int)g;
-  if (sweep_variant(d) == 2) {
+  if (var == 2) {
     *LD = d | 1;
     const size_t main = (size_t)(64 * (d | 1) + 4 * C * 64 + 64 * C) * sizeof(double);
     const size_t red = (size_t)std::max(4 * C * 2 * 64, 4 * 256) * sizeof(double);
@@ -519,8 +816,21 @@ static hipError_t pick_vec(const SweepArgs& A, int d, int nblocks, size_t lds, h
 }
 
 template <int FAM, int C>
-static hipError_t pick_tile(const SweepArgs& A, int d, int T, int nblocks, size_t lds, hipStream_t st) {
-  if (sweep_variant(d) == 2) {
+static hipError_t pick_tile(const SweepArgs& A, int64_t n, int d, int T, int nblocks, size_t lds, hipStream_t st) {
+  const int var = sweep_variant(n, d, C);
+  if (var == 3) {
+    if constexpr (C <= 4) {
+      static bool attr = false;
+      if (!attr) {
+        hipFuncSetAttribute((const void*)k_sweep3<FAM, C>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+      }
+      hipLaunchKernelGGL((k_sweep3<FAM, C>), dim3(nblocks), dim3(512), lds, st, A, A.LD);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
+  if (var == 2) {
     static bool attr = false;
     if (!attr) {
       hipFuncSetAttribute((const void*)k_sweep2<FAM, C>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -539,12 +849,12 @@ static hipError_t pick_tile(const SweepArgs& A, int d, int T, int nblocks, size_
 }
 
 template <int FAM>
-static hipError_t pick_c(const SweepArgs& A, int d, int T, int nblocks, size_t lds, hipStream_t st) {
+static hipError_t pick_c(const SweepArgs& A, int64_t n, int d, int T, int nblocks, size_t lds, hipStream_t st) {
   switch (A.C) {
-    case 1: return pick_tile<FAM, 1>(A, d, T, nblocks, lds, st);
-    case 2: return pick_tile<FAM, 2>(A, d, T, nblocks, lds, st);
-    case 4: return pick_tile<FAM, 4>(A, d, T, nblocks, lds, st);
-    case 8: return pick_tile<FAM, 8>(A, d, T, nblocks, lds, st);
+    case 1: return pick_tile<FAM, 1>(A, n, d, T, nblocks, lds, st);
+    case 2: return pick_tile<FAM, 2>(A, n, d, T, nblocks, lds, st);
+    case 4: return pick_tile<FAM, 4>(A, n, d, T, nblocks, lds, st);
+    case 8: return pick_tile<FAM, 8>(A, n, d, T, nblocks, lds, st);
   }
   return hipErrorInvalidValue;
 }
@@ -555,13 +865,13 @@ bool stk_sweep_supported(int C, int d) {
 }
 
 // Launch the sweep over `nsh` shards starting at shard0 (all with the same n, d geometry).
-hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, int nsh, int d, int T, int LD,
-                            int G, int Gs, size_t lds, const double* q, int C, int Dp, double* partial,
+hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, int nsh, int64_t n, int d, int T,
+                            int LD, int G, int Gs, size_t lds, const double* q, int C, int Dp, double* partial,
                             const int* req_step, int step_id, int* ran, hipStream_t st) {
   SweepArgs A{shards_dev, q, partial, req_step, step_id, C, Dp, G, LD, d + 2, shard0, Gs, ran};
   const int nblocks = nsh * G;
-  if (family == STK_LOGREG) return pick_c<STK_LOGREG>(A, d, T, nblocks, lds, st);
-  if (family == STK_LINREG) return pick_c<STK_LINREG>(A, d, T, nblocks, lds, st);
+  if (family == STK_LOGREG) return pick_c<STK_LOGREG>(A, n, d, T, nblocks, lds, st);
+  if (family == STK_LINREG) return pick_c<STK_LINREG>(A, n, d, T, nblocks, lds, st);
   return hipErrorInvalidValue;
 }
 

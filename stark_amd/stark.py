@@ -71,7 +71,8 @@ def _extract_to_matrix(extract):
 _CONTROL_KEYS = {"adapt_delta": "adapt_delta", "max_treedepth": "max_depth", "stepsize": "stepsize",
                  "adapt_gamma": "adapt_gamma", "adapt_kappa": "adapt_kappa", "adapt_t0": "adapt_t0",
                  "adapt_init_buffer": "adapt_init_buffer", "adapt_term_buffer": "adapt_term_buffer",
-                 "adapt_window": "adapt_window", "adapt_engaged": "adapt_engaged", "inv_metric": "inv_metric"}
+                 "adapt_window": "adapt_window", "adapt_engaged": "adapt_engaged", "inv_metric": "inv_metric",
+                 "stepsize_jitter": "stepsize_jitter"}
 
 
 def _unconstrain(family, data, init_dict):
@@ -103,8 +104,6 @@ def sampling_config(family, datas, **kw):
     control = dict(kw.pop("control", None) or {})
     if control.pop("metric", "diag_e") != "diag_e":
         raise NotImplementedError("only metric='diag_e' (Stan's default) is supported")
-    if float(control.pop("stepsize_jitter", 0.0)) != 0.0:
-        raise NotImplementedError("stepsize_jitter must be 0 (Stan's default)")
     cfg = dict(num_warmup=warmup, num_samples=it - warmup, chains=chains, seed=seed)
     for k, v in control.items():
         if k not in _CONTROL_KEYS:

@@ -30,10 +30,13 @@ def test_schools_lpgrad(ctx, orc):
             assert np.all(_rel(g[c], og) < RTOL_LP)
 
 
-@pytest.mark.parametrize("n,d", [(1, 1), (7, 3), (1000, 100), (4097, 50), (333, 129), (257, 300), (100, 700),
-                                 (5000, 2), (64, 65)])
+# shapes cover every sweep variant: v3 LDS-DMA ring (even d <= 104: partial last tile, one tile,
+# many chunks, d = 2), v2 (even d <= 128 beyond v3), v1 (odd or wide d)
+@pytest.mark.parametrize("n,d,C", [(1, 1, 5), (7, 3, 5), (1000, 100, 5), (4097, 50, 5), (333, 129, 5),
+                                   (257, 300, 5), (100, 700, 5), (5000, 2, 5), (64, 65, 5), (64, 100, 5),
+                                   (65, 104, 3), (20000, 100, 4), (3000, 120, 5), (1000, 100, 1), (777, 100, 2)])
 @pytest.mark.parametrize("family", ["logistic", "linear"])
-def test_regression_lpgrad(ctx, orc, family, n, d):
+def test_regression_lpgrad(ctx, orc, family, n, d, C):
     from stark_amd import engine
     rng = np.random.default_rng(n * 1000 + d)
     X = rng.uniform(-1.7, 1.7, (n, d))
@@ -47,7 +50,6 @@ def test_regression_lpgrad(ctx, orc, family, n, d):
         y = 0.3 + X @ beta + rng.normal(size=n)
         om = orc.Model(orc.FAM_LINREG, X=X, y=y)
     m = engine.Model(ctx, family, [{"x": X[: max(1, n // 3)], "y": y[: max(1, n // 3)]}, {"x": X, "y": y}])
-    C = 5
     q = rng.normal(0, 0.2, (C, om.D))
     if family == "logistic":
         q[0, 1:] = beta * 40     # large |eta| rows

@@ -52,8 +52,8 @@ def test_transition_matches_oracle_logistic(ctx, orc):
 
 
 # ---------------------------------------------------------------- adaptive run vs oracle twin
-@pytest.mark.parametrize("nw", [30, 150])
-def test_adaptive_run_tracks_oracle(ctx, orc, nw):
+@pytest.mark.parametrize("nw,jitter", [(30, 0.0), (150, 0.0), (30, 0.5)])
+def test_adaptive_run_tracks_oracle(ctx, orc, nw, jitter):
     """Full warmup (init_stepsize probes, dual averaging, Welford windows incl. the 15/75/10
     short-warmup split at nw=30) on the GPU and in the recursive oracle from the same seed:
     on a well-conditioned posterior (stable dynamics, so ulp-level differences between ocml
@@ -66,15 +66,21 @@ def test_adaptive_run_tracks_oracle(ctx, orc, nw):
     m = engine.Model(ctx, "logistic", [{"x": X, "y": y}])
     om = orc.Model(orc.FAM_LOGREG, X=X, y=y)
     ns, C = 20, 2
-    res = m.sampler(num_warmup=nw, num_samples=ns, chains=C, seed=2024, save_warmup=True)
+    res = m.sampler(num_warmup=nw, num_samples=ns, chains=C, seed=2024, save_warmup=True,
+                    stepsize_jitter=jitter)
     res.run()
     eps, im = res.adaptation()
     uq = res.unconstrained(0)
+    _, st = res.draws(0)
     for c in range(C):
-        o = om.run_chain(num_warmup=nw, num_samples=ns, seed=2024, gid=c)
+        o = om.run_chain(num_warmup=nw, num_samples=ns, seed=2024, gid=c, stepsize_jitter=jitter)
         err = np.abs(uq[c] - o["q"]).max(axis=1)
         if nw <= 30:     # whole run on the oracle path
             assert err.max() < 1e-8, err.max()
+            # per-transition step size (jittered around the nominal one when jitter > 0)
+            np.testing.assert_allclose(st[c * ns:(c + 1) * ns, 1], o["stats"][nw:, 1], rtol=1e-8)
+            if jitter:
+                assert np.ptp(st[c * ns:(c + 1) * ns, 1]) > 0
             np.testing.assert_allclose(eps[c], o["stepsize"], rtol=1e-8)
             np.testing.assert_allclose(im[c, :om.D], o["inv_metric"], rtol=1e-8)
         else:

@@ -92,9 +92,10 @@ def test_sampling_config_mapping():
     from stark_amd.stark import sampling_config
     datas = [{"J": 4, "y": [1, 2, 3, 4], "sigma": [1, 1, 1, 1]}]
     c = sampling_config("schools", datas, iter=5000, chains=1, n_jobs=1, seed=9,
-                        control={"adapt_delta": 0.9, "max_treedepth": 12})
+                        control={"adapt_delta": 0.9, "max_treedepth": 12, "stepsize_jitter": 0.3})
     assert c["num_warmup"] == 2500 and c["num_samples"] == 2500
     assert c["adapt_delta"] == 0.9 and c["max_depth"] == 12 and c["seed"] == 9
+    assert c["stepsize_jitter"] == 0.3
     c0 = sampling_config("schools", datas, iter=20, chains=2, init=0, seed=1)
     assert c0["init"].shape == (12,) and not c0["init"].any()
     ci = sampling_config("schools", datas, iter=20, chains=1, seed=1, init=[{"mu": 1.0, "tau": np.e}])

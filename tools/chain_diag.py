@@ -19,12 +19,13 @@ p.add_argument("--adapt", type=int, default=300)
 p.add_argument("--samples", type=int, default=100)
 p.add_argument("--init", default="random")
 p.add_argument("--init-r", type=float, default=2.0)
+p.add_argument("--jitter", type=float, default=0.0)
 a = p.parse_args()
 ctx = engine.Context(0)
 rps = int(a.rows) // a.shards
 m = engine.Model.synthetic(ctx, "logistic", a.shards, rps, a.d, data_seed=20240)
 kw = dict(num_warmup=a.adapt, num_samples=a.samples, chains=a.chains, seed=20241, save_warmup=True,
-          init_radius=a.init_r)
+          init_radius=a.init_r, stepsize_jitter=a.jitter)
 if a.init == "zero":
     kw["init"] = np.zeros(a.shards * a.chains * (a.d + 1))
 s = m.sampler(**kw)
