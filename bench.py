@@ -37,13 +37,16 @@ HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameter
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=1500)
+    p.add_argument("--steps", type=int, default=4000)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--rows", type=float, default=1e8, help="total rows N over all shards")
     p.add_argument("--d", type=int, default=100)
     p.add_argument("--shards", type=int, default=8)
     p.add_argument("--chains", type=int, default=4, help="chains per shard (share one data sweep)")
-    p.add_argument("--adapt-iters", type=int, default=300)
+    p.add_argument("--adapt-iters", type=int, default=100)
+    p.add_argument("--stepsize-jitter", type=float, default=0.5,
+                   help="Stan control stepsize_jitter; breaks the trajectory-length resonance of NUTS on "
+                        "this near-isotropic posterior (DESIGN.md section 4)")
     p.add_argument("--seed", type=int, default=20240)
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -117,7 +120,7 @@ def main():
     A, W, K = a.adapt_iters, a.warmup, a.steps
     total = A + W + K + 1          # enough sampling iterations that no chain finishes in the window
     sampler = model.sampler(num_warmup=A, num_samples=total - A, chains=a.chains, seed=a.seed + 1,
-                            shard_ids=shard_ids)
+                            shard_ids=shard_ids, stepsize_jitter=a.stepsize_jitter)
 
     def log(msg):
         if rank == 0:
@@ -126,11 +129,16 @@ def main():
     log(f"data generated: {spr} shards x {rows_per_shard} rows x d={a.d} in {t_gen:.1f}s "
         f"({model.device_bytes() / 1e9:.1f} GB on this GPU)")
     t = time.perf_counter()
-    for it in range(10, A + 10, 10):
-        sampler.run(min(it, A))
+    # One run to the end of warmup, in bounded step batches for progress lines: chains move
+    # independently and only wait for each other once, at iteration A.
+    while True:
+        sampler.run(A, max_steps=1000)
+        its = sampler.iterations()
         inf = sampler.info()
-        log(f"adaptation {min(it, A)}/{A}: {time.perf_counter() - t:.1f}s, leapfrogs/chain "
-            f"{inf['leapfrogs'] / max(1, spr * a.chains):.0f}")
+        log(f"adaptation: {time.perf_counter() - t:.1f}s, transitions per chain min/median "
+            f"{its.min()}/{int(np.median(its))} of {A}, leapfrogs/chain {inf['leapfrogs'] / max(1, spr * a.chains):.0f}")
+        if its.min() >= A:
+            break
     t_adapt = time.perf_counter() - t
     sampler.run(total, max_steps=W)
     log(f"warmup steps done; timing {K} steps")
@@ -222,7 +230,8 @@ def main():
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            if tj.get("rows_per_shard") == rows_per_shard and tj.get("d") == a.d and tj.get("hbm_bytes_per_shard_sweep"):
+            if (tj.get("kernel") == "k_sweep3" and tj.get("rows_per_shard") == rows_per_shard and tj.get("d") == a.d
+                    and tj.get("hbm_bytes_per_shard_sweep")):
                 # PMC pass of the same shard geometry (tools/pmc_traffic.py): FETCH_SIZE x2 per
                 # shard sweep, times the shards a launch swept on average
                 traffic = tj["hbm_bytes_per_shard_sweep"] * shard_sweeps / max(sweeps, 1)
@@ -230,7 +239,7 @@ def main():
             traffic = None
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-            "kernel": "k_sweep<LOGREG>", "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": bytes_per_launch}
+            "kernel": "k_sweep3<LOGREG,4>", "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": bytes_per_launch}
     cpu = None
     if not a.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(a.d, rows_per_shard, a.shards, a.cpu_baseline_seconds)
@@ -251,7 +260,8 @@ def main():
         "data": "synthetic (Philox in HBM, SURVEY 8d)",
         "config": {"workload": "bayesian logistic regression, 8 subposterior shards + consensus combine",
                    "rows": int(a.rows), "d": a.d, "shards": a.shards, "shards_per_gpu": spr,
-                   "chains_per_shard": a.chains, "adapt_iters": A, "parallelism": f"shard-dp{world}"},
+                   "chains_per_shard": a.chains, "adapt_iters": A, "stepsize_jitter": a.stepsize_jitter,
+                   "parallelism": f"shard-dp{world}"},
         "ess_per_sec": ess_ps,
         "min_ess": min_ess,
         "subposterior_min_ess_shard0": sub_ess,

@@ -20,7 +20,7 @@ p.add_argument("--write-csv", default=None)
 p.add_argument("--rows-per-shard", type=int, required=True)
 p.add_argument("--d", type=int, required=True)
 p.add_argument("--shards-per-gpu", type=int, required=True)
-p.add_argument("--kernel", default="k_sweep2")
+p.add_argument("--kernel", default="k_sweep3")
 p.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                              "profiles", "sweep_pmc.json"))
 a = p.parse_args()
