@@ -19,6 +19,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <set>
 #include <type_traits>
 
 namespace stk {
@@ -441,6 +442,9 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 #undef STK_VMCNT
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0xF70); }
+
 constexpr int S3_T = 64;          // rows per tile
 constexpr int S3_W = 8;           // waves per block
 constexpr int S3_MAXP = 7;        // pieces per lane in the forward: K <= 56
@@ -493,15 +497,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, in
 
 // ABL (micro-benchmark ablations only, tools/sweep_micro.hip; 0 in the product): bit 0 replaces
 // the residual's transcendentals by a linear stand-in, bit 1 skips the backward, bit 2 the forward.
-template <int FAM, int C, int ABL = 0>
-__global__ __launch_bounds__(512) void k_sweep3(SweepArgs A, int NB) {
+// KS, NBS: compile-time K (= d/2) and ring depth for the BASELINE shapes (d = 100, 50), so
+// the DMA issue unrolls and the steady-state wait is one immediate; 0 = runtime (any d).
+template <int FAM, int C, int ABL = 0, int KS = 0, int NBS = 0>
+__global__ __launch_bounds__(512) void k_sweep3(SweepArgs A, int NBrt) {
   constexpr int T = S3_T, NW = S3_W;
   const int shard = A.shard0 + blockIdx.x / A.G;
   const int chunk = blockIdx.x % A.G;
   if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
   if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
   const ShardDev sh = A.shards[shard];
-  const int d = sh.d, K = d >> 1;
+  const int d = sh.d, K = KS ? KS : (d >> 1), NB = NBS ? NBS : NBrt;
   const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
   const int64_t nt = (sh.n + T - 1) / T;
   const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
@@ -563,7 +569,13 @@ __global__ __launch_bounds__(512) void k_sweep3(SweepArgs A, int NB) {
   for (int t = 0; t < ntiles; ++t) {
     // own DMAs of sub-tile t retired; later sub-tiles (issued already) stay in flight
     const int later = std::min(NB - 2, ntiles - 1 - t);
-    wait_vmcnt(later * per_tile);
+    if constexpr (KS > 0) {
+      constexpr int PT = ((8 * 16 * KS + 1023) >> 10) + 1;
+      if (later == NBS - 2) wait_vm<(NBS - 2) * PT>();
+      else wait_vmcnt(later * PT);
+    } else {
+      wait_vmcnt(later * per_tile);
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): reads of slot t-1 are done
     __builtin_amdgcn_sched_barrier(0);
     if (t + NB - 1 < ntiles) issue(t + NB - 1);          // into slot (t-1) % NB
@@ -798,6 +810,12 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
   *lds_bytes = b;
 }
 
+// Raise a kernel's dynamic-LDS limit to the CU's 160 KiB, once per kernel.
+static void allow_big_lds(const void* kern) {
+  static std::set<const void*> done;
+  if (done.insert(kern).second) hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
 template <int FAM, int C, int T, int JPT, int VEC>
 static hipError_t launch_sweep_t(const SweepArgs& A, int nblocks, size_t lds, hipStream_t st) {
   static bool attr = false;
@@ -820,13 +838,14 @@ static hipError_t pick_tile(const SweepArgs& A, int64_t n, int d, int T, int nbl
   const int var = sweep_variant(n, d, C);
   if (var == 3) {
     if constexpr (C <= 4) {
-      static bool attr = false;
-      if (!attr) {
-        hipFuncSetAttribute((const void*)k_sweep3<FAM, C>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-      }
-      hipLaunchKernelGGL((k_sweep3<FAM, C>), dim3(nblocks), dim3(512), lds, st, A, A.LD);
-      return hipGetLastError();
+      auto go = [&](auto kern) {
+        allow_big_lds((const void*)kern);
+        hipLaunchKernelGGL(kern, dim3(nblocks), dim3(512), lds, st, A, A.LD);
+        return hipGetLastError();
+      };
+      if (d == 100 && A.LD == 3) return go(k_sweep3<FAM, C, 0, 50, 3>);
+      if (d == 50 && A.LD == 5) return go(k_sweep3<FAM, C, 0, 25, 5>);
+      return go(k_sweep3<FAM, C>);
     }
     return hipErrorInvalidValue;
   }

@@ -231,6 +231,7 @@ int main(int argc, char** argv) {
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       timeit(name, bytes, [&] { hipLaunchKernelGGL(kern, dim3(nsh * G), dim3(512), lds, st, A3, LD); });
     };
+    abl("v3 generic", k_sweep3<STK_LOGREG, 4, 0>);
     abl("v3 -trans", k_sweep3<STK_LOGREG, 4, 1>);
     abl("v3 -bwd", k_sweep3<STK_LOGREG, 4, 2>);
     abl("v3 -fwd", k_sweep3<STK_LOGREG, 4, 4>);
