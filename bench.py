@@ -32,6 +32,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_PEAK_TFS = 78.6    # MI355X fp64 matrix (= vector) spec, dense
+FP64_MEASURED_TFS = 46.0  # v_mfma_f64_16x16x4 back to back, 2+ waves/SIMD (tools/mfma_overlap.hip, profiles/)
 
 
 def parse():
@@ -42,7 +44,8 @@ def parse():
     p.add_argument("--rows", type=float, default=1e8, help="total rows N over all shards")
     p.add_argument("--d", type=int, default=100)
     p.add_argument("--shards", type=int, default=8)
-    p.add_argument("--chains", type=int, default=4, help="chains per shard (share one data sweep)")
+    p.add_argument("--chains", type=int, default=16,
+                   help="chains per shard; they share one data sweep (16: the fp64 MFMA sweep, X.[beta_1..beta_16])")
     p.add_argument("--adapt-iters", type=int, default=100)
     p.add_argument("--stepsize-jitter", type=float, default=0.5,
                    help="Stan control stepsize_jitter; breaks the trajectory-length resonance of NUTS on "
@@ -222,24 +225,39 @@ def main():
         return
 
     # ---- roofline of the dominant kernel (the data sweep)
+    # C = 16: k_sweepm, X.[beta_1..beta_16] on fp64 MFMA, bound by the fp64 pipe;
+    # C <= 4: k_sweep3 (VALU), bound by HBM.
+    mfma = a.chains == 16
+    kname = "k_sweepm" if mfma else "k_sweep3"
     bytes_per_shard = rows_per_shard * (8 * a.d + 4)        # X fp64 + y int32, once per sweep
     avg_ms = sweep_ms / max(sweeps, 1)
-    bytes_per_launch = bytes_per_shard * shard_sweeps / max(sweeps, 1)
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if sweeps else None
+    shards_per_launch = shard_sweeps / max(sweeps, 1)
+    bytes_per_launch = bytes_per_shard * shards_per_launch
+    flops_per_launch = 4.0 * rows_per_shard * a.d * a.chains * shards_per_launch   # fwd + bwd GEMMs
+    gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if sweeps else None
+    tfs = flops_per_launch / (avg_ms * 1e-3) / 1e12 if sweeps else None
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            if (tj.get("kernel") == "k_sweep3" and tj.get("rows_per_shard") == rows_per_shard and tj.get("d") == a.d
+            if (tj.get("kernel") == kname and tj.get("rows_per_shard") == rows_per_shard and tj.get("d") == a.d
                     and tj.get("hbm_bytes_per_shard_sweep")):
                 # PMC pass of the same shard geometry (tools/pmc_traffic.py): FETCH_SIZE x2 per
                 # shard sweep, times the shards a launch swept on average
-                traffic = tj["hbm_bytes_per_shard_sweep"] * shard_sweeps / max(sweeps, 1)
+                traffic = tj["hbm_bytes_per_shard_sweep"] * shards_per_launch
         except Exception:
             traffic = None
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-            "kernel": "k_sweep3<LOGREG,4>", "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": bytes_per_launch}
+    hbm = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": (gbs / HBM_PEAK_GBS) if gbs else None}
+    if mfma:
+        roof = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": (tfs / FP64_PEAK_TFS) if tfs else None, "traffic": traffic,
+                "kernel": f"k_sweepm<LOGREG> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
+                "algorithmic_flops_per_launch": flops_per_launch, "algorithmic_bytes_per_launch": bytes_per_launch,
+                "hbm": hbm, "fp64_measured_ceiling_tfs": FP64_MEASURED_TFS}
+    else:
+        roof = dict(bound="hbm", **{k: v for k, v in hbm.items()}, traffic=traffic,
+                    kernel=f"k_sweep3<LOGREG,{a.chains}>", avg_launch_ms=avg_ms,
+                    algorithmic_bytes_per_launch=bytes_per_launch)
     cpu = None
     if not a.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(a.d, rows_per_shard, a.shards, a.cpu_baseline_seconds)

@@ -422,7 +422,8 @@ int stk_log_density_grad(stk_model* m, int shard, const double* q, int32_t C, do
   } else {
     int T, LD, G;
     size_t lds;
-    const int Cb = C <= 1 ? 1 : (C <= 2 ? 2 : 4);   // the chain batch the sampler's sweep uses
+    // the chain batch the sampler's sweep uses: 16 (fp64 MFMA) when 16 or more points are asked for
+    const int Cb = C <= 1 ? 1 : (C <= 2 ? 2 : (C < 16 || !stk_sweep_supported(16, s.d) ? 4 : 16));
     stk_sweep_geometry(s.n, s.d, &T, &LD, &G, &lds, Cb);
     const int PW = s.d + 2;
     RC(ctx->scratch[0].ensure(sizeof(double) * (size_t)(m->nshards * Cb) * Dp));
@@ -496,7 +497,7 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   const int nch = stk_nch_for(m->Dmax);
   ARG_CHECK(nch > 0, "dimension %d too large (max 1024)", m->Dmax);
   if (m->family == STK_SCHOOLS) ARG_CHECK(nch <= 2, "8-schools supports J <= 126");
-  else ARG_CHECK(stk_sweep_supported(cfg->chains, m->d), "chains per shard must be 1, 2, 4 or 8 for regressions");
+  else ARG_CHECK(stk_sweep_supported(cfg->chains, m->d), "chains per shard must be 1, 2, 4, 8 or 16 (16: d <= 128) for regressions");
   stk_sampler* s = new stk_sampler();
   s->m = m;
   m->refs++;

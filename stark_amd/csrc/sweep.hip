@@ -432,11 +432,17 @@ __global__ __launch_bounds__(256, 2) void k_sweep2(SweepArgs A) {
 __device__ __forceinline__ void wait_vmcnt(int n) {
   // s_waitcnt encoding (gfx9): vmcnt [3:0] + [15:14], expcnt [6:4] = 7, lgkmcnt [11:8] = 15
 #define STK_VMCNT(N) case N: __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0xF70); break;
-  switch (n) {
+  switch (n) {   // vmcnt is 6 bits on gfx950: 0..63
     STK_VMCNT(0) STK_VMCNT(1) STK_VMCNT(2) STK_VMCNT(3) STK_VMCNT(4) STK_VMCNT(5) STK_VMCNT(6)
     STK_VMCNT(7) STK_VMCNT(8) STK_VMCNT(9) STK_VMCNT(10) STK_VMCNT(11) STK_VMCNT(12) STK_VMCNT(13)
     STK_VMCNT(14) STK_VMCNT(15) STK_VMCNT(16) STK_VMCNT(17) STK_VMCNT(18) STK_VMCNT(19) STK_VMCNT(20)
     STK_VMCNT(21) STK_VMCNT(22) STK_VMCNT(23) STK_VMCNT(24) STK_VMCNT(25) STK_VMCNT(26) STK_VMCNT(27)
+    STK_VMCNT(28) STK_VMCNT(29) STK_VMCNT(30) STK_VMCNT(31) STK_VMCNT(32) STK_VMCNT(33) STK_VMCNT(34)
+    STK_VMCNT(35) STK_VMCNT(36) STK_VMCNT(37) STK_VMCNT(38) STK_VMCNT(39) STK_VMCNT(40) STK_VMCNT(41)
+    STK_VMCNT(42) STK_VMCNT(43) STK_VMCNT(44) STK_VMCNT(45) STK_VMCNT(46) STK_VMCNT(47) STK_VMCNT(48)
+    STK_VMCNT(49) STK_VMCNT(50) STK_VMCNT(51) STK_VMCNT(52) STK_VMCNT(53) STK_VMCNT(54) STK_VMCNT(55)
+    STK_VMCNT(56) STK_VMCNT(57) STK_VMCNT(58) STK_VMCNT(59) STK_VMCNT(60) STK_VMCNT(61) STK_VMCNT(62)
+    STK_VMCNT(63)
     default: __builtin_amdgcn_s_waitcnt(0xF70); break;   // vmcnt(0)
   }
 #undef STK_VMCNT
@@ -682,6 +688,271 @@ __global__ __launch_bounds__(512) void k_sweep3(SweepArgs A, int NBrt) {
   }
 }
 
+// v4 sweep: 16 chains of a shard on fp64 MFMA (C = 16, d <= 128).
+//
+// With C chains sharing a shard, X.[beta_1 .. beta_C] is a dense GEMM; at C = 16 the sweep's
+// fp64 work (4*d*C flop per row, 8 flop per byte of X) needs ~60 % of the chip's fp64 rate
+// to keep up with HBM, which VALU FMAs fed from LDS cannot sustain but v_mfma_f64_16x16x4_f64
+// can: its operands come from registers, one f64 per lane.  One 256-thread block per CU, one
+// wave per SIMD; wave w owns 16-row sub-tiles u = w, w+4, ... of the chunk and moves them
+// with `buffer_load_dwordx4 ... lds` into a private ring of NB slots (no barrier in the main
+// loop, as v3).  Per sub-tile, with lane l, lr = l & 15, lh = l >> 4:
+//   forward   eta[16 rows][16 chains] = X_tile . B: k-step s, lane group lh reads column
+//             lh*KF + s of row lr (A operand) against beta_lr[lh*KF + s] (B operand, held
+//             in registers for the whole launch): KF = ceil(d/4) MFMAs into two accumulators;
+//             lane l ends with eta[row lh + 4i][chain lr], i = 0..3;
+//   residual  Stan's bernoulli_logit cutoffs / the normal residual on those 4 (row, chain)
+//             pairs, in registers;
+//   backward  G[16 cols][16 chains] += X_tile^T . d_eta for each 16-column tile t: k-step s
+//             (rows 4s .. 4s+3) takes the residual's register i = s as its B operand as is
+//             (the D layout of the forward IS the B layout of the backward: no shuffle) and
+//             column 16t + lr of row lh + 4s as A: 4 MFMAs per column tile.
+// Columns past d are clamped reads against zero beta (forward) or discarded outputs
+// (backward).  Chunks, partial rows and the chunk-order reduction are those of v3, so the
+// gradient is bitwise independent of shard placement.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int SM_W = 4;                 // waves per block (one per SIMD)
+constexpr int SM_R = 16;                // rows per wave sub-tile = MFMA M (forward) and K (backward)
+constexpr int SM_C = 16;                // chains per launch row = MFMA N
+constexpr int SM_MINB = 2;              // blocks per CU: two waves per SIMD (fp64 MFMA issue from one wave tops out at ~75 %)
+__host__ __device__ constexpr int sweepm_slot_bytes(int d) { return SM_R * d * 8 + 128; }
+
+__device__ __forceinline__ dbl4 mfma_f64(double a, double b, dbl4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Table-driven softplus for the fp64-bound v4 residual (the fp64 MFMA and fp64 VALU share one
+// pipe on gfx950, so every f64 instruction of the residual costs MFMA time; ocml's exp + log
+// + the correction take ~105 instructions per (row, chain), this ~45).  Tables in LDS:
+//   tab[0 .. 64)          T_j = 2^(j/64)
+//   tab[64 + 2j], +1      c_j = 1/(1 + (j + 1/2)/128) (c_0 = 1), l_j = -log(c_j), j < 128
+// exp(x): x = n ln2/64 + r, |r| <= ln2/128, e^r by degree 5 (rel. error < 4e-17), times
+//         T_{n mod 64}, scaled by 2^(n div 64) (v_ldexp_f64);
+// log(u): u = 2^k m, m in [1, 2), r = m c_j - 1 (|r| <= 1/128; exact for j = 0, so log(u)
+//         keeps its relative accuracy as u -> 1), log(1+r) = r q(r), q of degree 6.
+// Worst relative error of the softplus term over |x| <= 20: 1e-14 (numpy/mpmath check of the
+// same formulas); the bar is 1e-10 (tests/test_gpu_kernels.py).
+constexpr int SP_TAB = 64 + 2 * 128;
+__device__ void softplus_tables_init(double* tab) {
+  for (int i = threadIdx.x; i < SP_TAB; i += blockDim.x) {
+    double v;
+    if (i < 64) {
+      v = exp2((double)i / 64.0);
+    } else {
+      const int j = (i - 64) >> 1;
+      const double c = j == 0 ? 1.0 : 1.0 / (1.0 + (j + 0.5) / 128.0);
+      v = ((i - 64) & 1) ? -log(c) : c;
+    }
+    tab[i] = v;
+  }
+}
+
+// e = exp(-ntt); lmid = log1p(e) (Stan's middle branch); w = e / (1 + e)
+__device__ __forceinline__ void softplus_tab(double ntt, const double* tab, double* e_out, double* lmid, double* w) {
+  constexpr double INV_L = 92.33248261689366;              // 64 / ln 2
+  constexpr double L_HI = 0.010830417275428772;            // ln2/64 rounded to 21 bits: n * L_HI is exact
+  constexpr double L_LO = 7.420820373486988e-09;           // ln2/64 - L_HI
+  constexpr double LN2 = 0.69314718055994530942;
+  const double x = fmin(fmax(-ntt, -800.0), 800.0);
+  const double n = __builtin_rint(x * INV_L);
+  const int ni = (int)n;
+  double r = fma(-n, L_HI, x);
+  r = fma(-n, L_LO, r);
+  double p = fma(fma(fma(fma(fma(1.0 / 120.0, r, 1.0 / 24.0), r, 1.0 / 6.0), r, 0.5), r, 1.0), r, 1.0);
+  const double e = __builtin_amdgcn_ldexp(tab[ni & 63] * p, ni >> 6);
+  const double u = 1.0 + e;
+  const double m2 = 2.0 * __builtin_amdgcn_frexp_mant(u);
+  const int k = __builtin_amdgcn_frexp_exp(u) - 1;
+  const int j = (int)((uint32_t)(__builtin_bit_cast(uint64_t, m2) >> 45) & 127u);
+  const dbl2 cl = *reinterpret_cast<const dbl2*>(tab + 64 + 2 * j);
+  const double rl = fma(m2, cl.x, -1.0);
+  double q = fma(fma(fma(fma(fma(fma(1.0 / 7.0, rl, -1.0 / 6.0), rl, 1.0 / 5.0), rl, -0.25), rl, 1.0 / 3.0), rl, -0.5), rl, 1.0);
+  const double lg = fma((double)k, LN2, fma(rl, q, cl.y));
+  double ri = __builtin_amdgcn_rcp(u);
+  ri = fma(ri, fma(-u, ri, 1.0), ri);
+  ri = fma(ri, fma(-u, ri, 1.0), ri);
+  *e_out = e;
+  *lmid = lg - ((u - 1.0) - e) * ri;
+  *w = e * ri;
+}
+
+// ABL (micro-benchmark ablations only): bit 0 linear residual stand-in, bit 1 no backward,
+// bit 2 no forward.  KFS/JTS: compile-time KF / JT for the BASELINE shapes (0 = runtime).
+template <int FAM, int KFS = 0, int JTS = 0, int ABL = 0, int MINB = SM_MINB>
+__global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
+  constexpr int C = SM_C, NW = SM_W;
+  constexpr int KFM = KFS ? KFS : 32, JTM = JTS ? JTS : 8;
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d;
+  const int KF = KFS ? KFS : (d + 3) >> 2;
+  const int JT = JTS ? JTS : (d + 15) >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + 63) / 64;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * 64, r1 = std::min<int64_t>(sh.n, t1 * 64);
+  const int nrows = (int)(r1 - r0);
+  const int nsub = (nrows + SM_R - 1) / SM_R;
+  const int mine = nsub > w ? (nsub - w + NW - 1) / NW : 0;   // own sub-tiles u = w + NW*k
+  constexpr int YB = (FAM == STK_LOGREG) ? 4 : 8;
+  const int SBX = SM_R * d * 8;
+  const int SS = sweepm_slot_bytes(d);
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const ring = reinterpret_cast<char*>(lds) + (size_t)w * NB * SS;
+  double* const sptab = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * NB * SS);
+  if constexpr (FAM == STK_LOGREG) {
+    softplus_tables_init(sptab);
+    __syncthreads();
+  }
+
+  // ---- chain lr's beta fragments (B operand of the forward), alpha, 1/sigma
+  const double* qc = A.q + ((size_t)shard * C + lr) * A.Dp;
+  double bf[KFM];
+#pragma unroll
+  for (int s = 0; s < KFM; ++s) {
+    const int col = lh * KF + s;
+    bf[s] = (s < KF && col < d) ? qc[1 + col] : 0.0;
+  }
+  const double alpha = qc[0];
+  const double inv_s = (FAM == STK_LINREG) ? exp(-qc[d + 1]) : 0.0;
+  __builtin_amdgcn_s_waitcnt(0xF70);                      // ordinary loads retired before the DMAs start
+
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
+  const void* ybase = (FAM == STK_LOGREG) ? (const void*)(sh.yi + r0) : (const void*)(sh.y + r0);
+  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(ybase, (int64_t)nrows * YB);
+  const int nx = (SBX + 1023) >> 10;
+  const int last_lanes = (SBX - ((nx - 1) << 10)) >> 4;
+  const int per_tile = nx + 1;
+  auto issue = [&](int k) {
+    char* sl = ring + (size_t)(k % NB) * SS;
+    const int u = w + NW * k;
+    const int xoff = u * SBX;
+    for (int j = 0; j < nx - 1; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(sl + j * 1024), 16, lane * 16, xoff + j * 1024, 0, 0);
+    if (lane < last_lanes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(sl + (nx - 1) * 1024), 16, lane * 16,
+                                               xoff + (nx - 1) * 1024, 0, 0);
+    if (lane < SM_R * YB / 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_vptr)(sl + SBX), 4, lane * 4, u * SM_R * YB, 0, 0);
+  };
+
+  dbl4 gacc[JTM];
+#pragma unroll
+  for (int t = 0; t < JTM; ++t) gacc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double lpa = 0.0, gaa = 0.0;
+
+  // Ring of NB slots per wave: sub-tiles k+1 .. k+NB-1 are in flight while sub-tile k is
+  // computed (NB = 1: the DMA of sub-tile k is issued when sub-tile k-1 is done, and the
+  // other waves of the SIMD -- two blocks per CU -- cover its latency).
+  for (int k = 0; k < NB - 1 && k < mine; ++k) issue(k);
+  for (int k = 0; k < mine; ++k) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): reads of slot k-1 are done
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + NB - 1 < mine) issue(k + NB - 1);            // into slot (k-1) % NB
+    wait_vmcnt(std::max(0, std::min(NB - 2, mine - 1 - k)) * per_tile);   // own DMAs of sub-tile k retired
+    __builtin_amdgcn_sched_barrier(0);
+    const char* sl = ring + (size_t)(k % NB) * SS;
+    const double* xs = reinterpret_cast<const double*>(sl);
+    const int rv = std::min(SM_R, nrows - SM_R * (w + NW * k));
+
+    // ---- forward: eta[row lh + 4i][chain lr] (without alpha)
+    dbl4 e0 = {0.0, 0.0, 0.0, 0.0}, e1 = {0.0, 0.0, 0.0, 0.0};
+    if constexpr (!(ABL & 4)) {
+      const double* xrow = xs + lr * d;
+#pragma unroll
+      for (int s = 0; s < KFM; ++s) {
+        if (s < KF) {
+          const double a = xrow[std::min(lh * KF + s, d - 1)];
+          if (s & 1) e1 = mfma_f64(a, bf[s], e1);
+          else e0 = mfma_f64(a, bf[s], e0);
+        }
+      }
+    }
+    const dbl4 eta4 = e0 + e1;
+
+    // ---- residual on (row lh + 4i, chain lr)
+    double de[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = lh + 4 * i;
+      const bool valid = row < rv;
+      const double eta = eta4[i] + alpha;
+      double dv, lt;
+      if constexpr (ABL & 1) {
+        const int32_t yv = *reinterpret_cast<const int32_t*>(sl + SBX + row * 4);
+        dv = (2.0 * yv - 1.0) - 0.25 * eta;
+        lt = -dv * dv;
+      } else if constexpr (FAM == STK_LOGREG) {
+        // Stan's bernoulli_logit: ntt > 20 -> -exp(-ntt); ntt < -20 -> ntt; else -log1p(exp(-ntt))
+        const int32_t yv = *reinterpret_cast<const int32_t*>(sl + SBX + row * 4);
+        const double sgn = 2.0 * yv - 1.0;
+        const double ntt = sgn * eta;
+        double e, lm, wt;
+        softplus_tab(ntt, sptab, &e, &lm, &wt);
+        const bool hi = ntt > 20.0, lo = ntt < -20.0;
+        lt = hi ? -e : (lo ? ntt : -lm);
+        dv = sgn * (hi ? e : (lo ? 1.0 : wt));
+      } else {
+        const double yv = *reinterpret_cast<const double*>(sl + SBX + row * 8);
+        const double z = (yv - eta) * inv_s;
+        lt = z * z;
+        dv = z * inv_s;
+      }
+      dv = valid ? dv : 0.0;
+      lpa += valid ? lt : 0.0;
+      gaa += dv;
+      de[i] = dv;
+    }
+
+    // ---- backward (s outer: JT independent accumulators between dependent MFMAs)
+    if constexpr (!(ABL & 2)) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int t = 0; t < JTM; ++t) {
+          if (t < JT) gacc[t] = mfma_f64(xs[(lh + 4 * s) * d + std::min(16 * t + lr, d - 1)], de[s], gacc[t]);
+        }
+      }
+    }
+  }
+
+  // ---- fixed-order block reduction -> one partial row per chain
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __syncthreads();
+  double* red = lds;                                   // [NW][JT*16 columns][16 chains]
+  const int JC = JT * 16;
+#pragma unroll
+  for (int t = 0; t < JTM; ++t) {
+    if (t < JT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[((size_t)w * JC + 16 * t + lh + 4 * i) * 16 + lr] = gacc[t][i];
+    }
+  }
+  double* red2 = red + (size_t)NW * JC * 16;           // [NW][64 lanes][lp, g_alpha]
+  red2[(size_t)tid * 2 + 0] = lpa;
+  red2[(size_t)tid * 2 + 1] = gaa;
+  __syncthreads();
+  double* out = A.partial + ((size_t)shard * A.Gs + chunk) * C * A.PW;
+  for (int i = tid; i < C * d; i += NW * 64) {
+    const int c = i / d, j = i % d;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww) v += red[((size_t)ww * JC + j) * 16 + c];
+    out[(size_t)c * A.PW + 1 + j] = v;
+  }
+  if (tid < 2 * C) {          // chain c: lanes h*16 + c of every wave, in (wave, h) order
+    const int c = tid >> 1, kind = tid & 1;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww)
+      for (int h = 0; h < 4; ++h) v += red2[(size_t)(ww * 64 + h * 16 + c) * 2 + kind];
+    out[(size_t)c * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
+}
+
 // Sum chunk partials in chunk order and finish the family's lp / gradient.
 // grid (nshards*C, ceil(PW/64)), 256 threads: 4 waves split the chunks, fixed combine order.
 template <int FAM>
@@ -753,7 +1024,17 @@ static int sweep3_nb(int d, int C) {
   return std::min(nb, 5);
 }
 
+// Ring depth of v4 (C = 16): slots of 16 rows per wave that fit SM_MINB blocks per CU, at most 6,
+// DMAs in flight <= 63 (d = 100: NB = 1, two blocks per CU).
+static int sweepm_nb(int d, int minb = SM_MINB) {
+  int nb = std::min(6, (160 * 1024 / minb - SP_TAB * 8) / (SM_W * sweepm_slot_bytes(d)));
+  const int pt = ((SM_R * d * 8 + 1023) >> 10) + 1;
+  while (nb > 2 && (nb - 2) * pt > 63) --nb;
+  return nb;
+}
+
 static int sweep_variant(int64_t n, int d, int C) {
+  if (C == SM_C) return (d <= 128 && sweepm_nb(d) >= 1 && (n * d * 8) / 512 < ((int64_t)1 << 30)) ? 4 : 0;
   const int f = sweep_forced();
   const bool v3ok = d % 2 == 0 && d / 2 <= S3_KMAX && (C == 1 || C == 2 || C == 4) && sweep3_nb(d, C) >= 3 &&
                     (n * d * 8) / 512 < ((int64_t)1 << 30);
@@ -766,6 +1047,21 @@ static int sweep_variant(int64_t n, int d, int C) {
 
 void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_bytes, int C) {
   const int var = sweep_variant(n, d, C);
+  if (var == 4) {
+    const int64_t nt = (n + 63) / 64;
+    int64_t g = (nt + 7) / 8;            // >= 8 tiles of 64 rows per chunk (as v3)
+    if (g > 512) g = 512;
+    if (g < 1) g = 1;
+    const int nb = sweepm_nb(d);
+    *T = 64;
+    *LD = nb;
+    *G = (int)g;
+    const int JT = (d + 15) / 16;
+    const size_t ring = (size_t)SM_W * nb * sweepm_slot_bytes(d) + SP_TAB * sizeof(double);
+    const size_t red = ((size_t)SM_W * JT * 16 * 16 + (size_t)SM_W * 64 * 2) * sizeof(double);
+    *lds_bytes = std::max(ring, red);
+    return;
+  }
   if (var == 3) {
     const int64_t nt = (n + S3_T - 1) / S3_T;
     int64_t g = (nt + 7) / 8;            // >= 8 tiles per chunk
@@ -868,7 +1164,20 @@ static hipError_t pick_tile(const SweepArgs& A, int64_t n, int d, int T, int nbl
 }
 
 template <int FAM>
+static hipError_t launch_sweepm(const SweepArgs& A, int d, int nblocks, size_t lds, hipStream_t st) {
+  auto go = [&](auto kern) {
+    allow_big_lds((const void*)kern);
+    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A, A.LD);
+    return hipGetLastError();
+  };
+  if (d == 100) return go(k_sweepm<FAM, 25, 7>);
+  if (d == 50) return go(k_sweepm<FAM, 13, 4>);
+  return go(k_sweepm<FAM>);
+}
+
+template <int FAM>
 static hipError_t pick_c(const SweepArgs& A, int64_t n, int d, int T, int nblocks, size_t lds, hipStream_t st) {
+  if (A.C == SM_C) return sweep_variant(n, d, A.C) == 4 ? launch_sweepm<FAM>(A, d, nblocks, lds, st) : hipErrorInvalidValue;
   switch (A.C) {
     case 1: return pick_tile<FAM, 1>(A, n, d, T, nblocks, lds, st);
     case 2: return pick_tile<FAM, 2>(A, n, d, T, nblocks, lds, st);
@@ -879,6 +1188,7 @@ static hipError_t pick_c(const SweepArgs& A, int64_t n, int d, int T, int nblock
 }
 
 bool stk_sweep_supported(int C, int d) {
+  if (C == SM_C) return d >= 1 && d <= 128;
   if (!(C == 1 || C == 2 || C == 4 || C == 8)) return false;
   return d >= 1 && d <= 1024;
 }

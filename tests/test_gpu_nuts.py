@@ -122,14 +122,14 @@ def test_schools_4096_chains_exact_moments(ctx, orc):
     s.close()
 
 
-def test_linear_regression_closed_form(ctx, orc):
+@pytest.mark.parametrize("C", [8, 16])      # 16: the fp64 MFMA sweep (v4)
+def test_linear_regression_closed_form(ctx, orc, C):
     from stark_amd import engine
     rng = np.random.default_rng(8)
     n, d = 2000, 5
     X = rng.uniform(-1.7, 1.7, (n, d))
     y = 0.7 + X @ rng.normal(0, 0.5, d) + 1.3 * rng.normal(size=n)
     m = engine.Model(ctx, "linear", [{"x": X, "y": y}])
-    C = 8
     s = m.sampler(num_warmup=500, num_samples=1000, chains=C, seed=21)
     s.run()
     uq = s.unconstrained(0)
@@ -143,14 +143,15 @@ def test_linear_regression_closed_form(ctx, orc):
     s.close()
 
 
-def test_logistic_matches_oracle_moments(ctx, orc):
+@pytest.mark.parametrize("C", [8, 16])
+def test_logistic_matches_oracle_moments(ctx, orc, C):
     from stark_amd import engine
     rng = np.random.default_rng(12)
     n, d = 3000, 4
     X = rng.uniform(-1.7, 1.7, (n, d))
     y = (rng.uniform(size=n) < 1 / (1 + np.exp(-(0.2 + X @ rng.normal(0, 0.6, d))))).astype(np.int32)
     m = engine.Model(ctx, "logistic", [{"x": X, "y": y}])
-    s = m.sampler(num_warmup=500, num_samples=1000, chains=8, seed=5)
+    s = m.sampler(num_warmup=500, num_samples=1000, chains=C, seed=5)
     s.run()
     g = s.unconstrained(0)
     om = orc.Model(orc.FAM_LOGREG, X=X, y=y)
@@ -165,10 +166,11 @@ def test_logistic_matches_oracle_moments(ctx, orc):
 
 
 # ---------------------------------------------------------------- reproducibility
-def test_bitwise_reproducible_and_resumable(ctx):
+@pytest.mark.parametrize("C", [2, 16])
+def test_bitwise_reproducible_and_resumable(ctx, C):
     from stark_amd import engine
     m = engine.Model.synthetic(ctx, "logistic", 2, 5000, 8, data_seed=3)
-    cfg = dict(num_warmup=60, num_samples=40, chains=2, seed=11)
+    cfg = dict(num_warmup=60, num_samples=40, chains=C, seed=11)
     a = m.sampler(**cfg)
     a.run()
     b = m.sampler(**cfg)
@@ -183,11 +185,12 @@ def test_bitwise_reproducible_and_resumable(ctx):
     b.close()
 
 
-def test_shard_placement_independent(ctx):
+@pytest.mark.parametrize("C", [4, 16])
+def test_shard_placement_independent(ctx, C):
     """1 GPU holding 4 shards == 4 GPUs holding one shard each (same global shard ids)."""
     from stark_amd import engine
     rows, d = 3000, 10
-    cfg = dict(num_warmup=50, num_samples=30, chains=4, seed=5)
+    cfg = dict(num_warmup=50, num_samples=30, chains=C, seed=5)
     full = engine.Model.synthetic(ctx, "logistic", 4, rows, d, data_seed=8)
     ref = full.sample(**cfg)
     for k in (1, 3):

@@ -51,6 +51,17 @@ __global__ __launch_bounds__(256) void k_stream(const ShardDev* shards, int G, d
   if (acc.x == 12345.678) sink[blockIdx.x] = acc.y;   // never true: keeps the loads
 }
 
+// fp64 MFMA issue rate: 4 independent accumulators per wave, back to back.
+__global__ __launch_bounds__(256) void k_mfma_peak(double* sink, int iters) {
+  dbl4 acc[4] = {};
+  const double a = threadIdx.x * 1e-3, b = 1.0 + threadIdx.x * 1e-6;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = mfma_f64(a, b, acc[j]);
+  }
+  if (acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3] == 12345.678) sink[blockIdx.x] = 1.0;
+}
+
 template <int NT_ROWS>
 __global__ __launch_bounds__(256, 2) void k_skeleton(SweepArgs A, double* sink) {
   constexpr int T = NT_ROWS, NT = 256;
@@ -149,7 +160,7 @@ int main(int argc, char** argv) {
   const int nsh = argc > 2 ? atoi(argv[2]) : 4;
   const int d = argc > 3 ? atoi(argv[3]) : 100;
   const int reps = argc > 4 ? atoi(argv[4]) : 10;
-  const int C = 4, Dp = (d + 1 + 7) / 8 * 8;
+  const int C = argc > 5 ? atoi(argv[5]) : 4, Dp = (d + 1 + 7) / 8 * 8;
   hipStream_t st;
   CK(hipStreamCreate(&st));
   std::vector<ShardDev> sh(nsh);
@@ -237,6 +248,40 @@ int main(int argc, char** argv) {
     abl("v3 -fwd", k_sweep3<STK_LOGREG, 4, 4>);
     abl("v3 -t-b", k_sweep3<STK_LOGREG, 4, 3>);
     abl("v3 -all", k_sweep3<STK_LOGREG, 4, 7>);
+  }
+  if (sweep_variant(rows, d, C) == 4 && d == 100) {
+    SweepArgs A4{sh_d, q, partial, nullptr, 0, C, Dp, G, LD, d + 2, 0, G, nullptr};
+    auto abl = [&](const char* name, auto kern) {
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      timeit(name, bytes, [&] { hipLaunchKernelGGL(kern, dim3(nsh * G), dim3(256), lds, st, A4, LD); });
+    };
+    abl("v4 generic", k_sweepm<STK_LOGREG, 0, 0, 0>);
+    {   // one block per CU, 3-slot rings
+      const int nb1 = sweepm_nb(d, 1);
+      SweepArgs A1 = A4;
+      A1.LD = nb1;
+      const size_t l1 = std::max((size_t)SM_W * nb1 * sweepm_slot_bytes(d) + SP_TAB * 8, lds);
+      auto kern = k_sweepm<STK_LOGREG, 25, 7, 0, 1>;
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      timeit("v4 1blk nb3", bytes, [&] { hipLaunchKernelGGL(kern, dim3(nsh * G), dim3(256), l1, st, A1, nb1); });
+    }
+    abl("v4 -trans", k_sweepm<STK_LOGREG, 25, 7, 1>);
+    abl("v4 -bwd", k_sweepm<STK_LOGREG, 25, 7, 2>);
+    abl("v4 -fwd", k_sweepm<STK_LOGREG, 25, 7, 4>);
+    abl("v4 -all", k_sweepm<STK_LOGREG, 25, 7, 7>);
+    const double fl = 4.0 * d * C * (double)rows * nsh;   // algorithmic fp64 flops of one sweep
+    timeit("v4 flops", fl, [&] {
+      CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st));
+    });
+    printf("  (v4 flops line: 'GB/s' column = GFLOP/s of the sweep's 4*d*C flop per row)\n");
+    for (int wpb = 1; wpb <= 4; wpb *= 2) {
+      const int iters = 2000, blocks = 256 * 4;
+      char name[32];
+      snprintf(name, sizeof name, "mfma f64 w%d", wpb);
+      timeit(name, (double)blocks * wpb * iters * 4 * 2048.0, [&] {
+        hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(64 * wpb), 0, st, sink, iters);
+      });
+    }
   }
   timeit("sweep", bytes, [&] {
     CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st));
