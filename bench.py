@@ -13,10 +13,13 @@ back by each other: each runs its own trajectories, transitions and draws.  Time
   sync+barrier.
 `value` = chain-gradient evaluations of all ranks in the timed region / max-over-ranks time
 (every chain evaluates one gradient per step, so = chains * K / time).
-ESS/s: every chain contributes the M transitions it completed inside the timed window
-(M = the minimum over chains, so shards align); the consensus combine of those draws runs on
-the GPU after one all-gather; ESS/s = min over non-lp__ parameters of the combined draws'
-ESS / the timed window.
+ESS/s: the transitions every chain completed inside the timed window, rank-paired across
+shards (combined chain k = the chain with the k-th most window transitions of each shard,
+cut to the fewest of them, so draw i of every shard is combined with draw i of the others);
+the consensus combine runs on the GPU after one all-gather; ESS/s = min over non-lp__
+parameters of the combined draws' ESS (sum over combined chains of Stan's single-chain
+estimator) / the timed window.  ess_per_sec_equal_length: Stan's multi-chain estimator on
+every chain cut to the shortest (conservative).
 
 Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
 """
@@ -46,7 +49,8 @@ def parse():
     p.add_argument("--shards", type=int, default=8)
     p.add_argument("--chains", type=int, default=16,
                    help="chains per shard; they share one data sweep (16: the fp64 MFMA sweep, X.[beta_1..beta_16])")
-    p.add_argument("--adapt-iters", type=int, default=100)
+    p.add_argument("--adapt-iters", type=int, default=150,
+                   help="Stan warmup iterations (>= 150: a metric window after the initial transient)")
     p.add_argument("--stepsize-jitter", type=float, default=0.5,
                    help="Stan control stepsize_jitter; breaks the trajectory-length resonance of NUTS on "
                         "this near-isotropic posterior (DESIGN.md section 4)")
@@ -171,7 +175,6 @@ def main():
     shard_sweeps = i1["shard_sweeps"] - i0["shard_sweeps"]
     sweep_ms = i1["sweep_ms"] - i0["sweep_ms"]
     done_in_window = it1 - it0                       # transitions completed per chain
-    m_local = int(done_in_window.min())
     eps, _ = sampler.adaptation()
     if dist:
         v = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -180,23 +183,31 @@ def main():
         g = torch.tensor([grads, leaps], dtype=torch.float64, device="cuda")
         dist.all_reduce(g, op=dist.ReduceOp.SUM)
         grads, leaps = int(g[0].item()), int(g[1].item())
-        mm = torch.tensor([m_local], dtype=torch.int64, device="cuda")
-        dist.all_reduce(mm, op=dist.ReduceOp.MIN)
-        M = int(mm.item())
-    else:
-        M = m_local
 
-    # ---- draws completed inside the window (first M per chain) -> consensus -> ESS
+    # ---- draws completed inside the window -> consensus -> ESS.
+    # The consensus average pairs draw i of every shard; chains are exchangeable, so combined
+    # chain k joins the chain with the k-th most window transitions of every shard and keeps
+    # M_k = the fewest of those (no draw is made up, chain boundaries align across shards).
+    C = a.chains
     P = model.P[0]
+    counts = {shard_ids[s]: done_in_window[s * C:(s + 1) * C].astype(int).tolist() for s in range(spr)}
+    if dist:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, counts)
+        counts = {k_: v_ for dct in gathered for k_, v_ in dct.items()}
+    order = {sh: np.argsort(-np.asarray(cnt), kind="stable") for sh, cnt in counts.items()}
+    Mk = np.array([min(counts[sh][order[sh][k]] for sh in counts) for k in range(C)])
     local = {}
+    per = total - A
     for s in range(spr):
         dr, _ = sampler.draws(s)
-        per = total - A
+        sh = shard_ids[s]
         cols = []
-        for c in range(a.chains):
-            first = it0[s * a.chains + c] - A       # sampling index of the first window transition
-            cols.append(np.arange(c * per + first, c * per + first + M))
-        local[shard_ids[s]] = np.ascontiguousarray(dr[:, np.concatenate(cols)]) if M > 0 else None
+        for k in range(C):
+            c = order[sh][k]
+            first = it0[s * C + c] - A               # sampling index of the chain's first window transition
+            cols.append(np.arange(c * per + first, c * per + first + Mk[k]))
+        local[sh] = np.ascontiguousarray(dr[:, np.concatenate(cols)]) if Mk.sum() > 0 else None
     if dist:
         allp = [None] * a.shards
         gathered = [None] * world
@@ -206,14 +217,28 @@ def main():
                 allp[k_] = v_
     else:
         allp = [local[k_] for k_ in range(a.shards)]
-    ess_ps, min_ess, sub_ess = None, None, None
-    if rank == 0 and M >= 4:
-        sub_ess = float(np.nanmin(diagnostics.ess_matrix(allp[0][:-1], a.chains)))
-        if a.chains * M > P + 1:
-            comb, used = engine.consensus(allp, ctx)
-            e = diagnostics.ess_matrix(comb[:-1], a.chains)     # drop lp__
-            min_ess = float(np.nanmin(e))
-            ess_ps = min_ess / elapsed
+
+    def ess_rows(x, equal):
+        """min over parameter rows of the ESS of x (P' x sum(Mk), chain segments of lengths Mk):
+        equal: Stan's multi-chain estimator on every segment cut to min(Mk);
+        else: sum over segments (M_k >= 4) of Stan's single-chain estimator (independent chains)."""
+        off = np.concatenate([[0], np.cumsum(Mk)])
+        out = []
+        for p in range(x.shape[0]):
+            if equal:
+                m = int(Mk.min())
+                out.append(diagnostics.ess(np.stack([x[p, off[k]:off[k] + m] for k in range(C)])))
+            else:
+                out.append(sum(diagnostics.ess(x[p, off[k]:off[k + 1]]) for k in range(C) if Mk[k] >= 4))
+        return float(np.nanmin(out))
+
+    ess_ps, min_ess, ess_eq, sub_ess = None, None, None, None
+    if rank == 0 and Mk.sum() > P + 1 and Mk.max() >= 4:
+        sub_ess = ess_rows(allp[0][:-1], False)
+        comb, used = engine.consensus(allp, ctx)
+        min_ess = ess_rows(comb[:-1], False)                     # drop lp__
+        ess_eq = ess_rows(comb[:-1], True) if Mk.min() >= 4 else None
+        ess_ps = min_ess / elapsed
     info = sampler.info()
     sampler.close()
 
@@ -282,9 +307,13 @@ def main():
                    "parallelism": f"shard-dp{world}"},
         "ess_per_sec": ess_ps,
         "min_ess": min_ess,
+        "ess_method": "min over parameters (lp__ excluded) of the consensus draws completed in the timed window; "
+                      "sum over rank-paired chains of Stan's single-chain ESS",
+        "ess_per_sec_equal_length": (ess_eq / elapsed) if ess_eq else None,
         "subposterior_min_ess_shard0": sub_ess,
         "transitions_per_chain_in_window": {"min": int(done_in_window.min()), "median": float(np.median(done_in_window)),
-                                            "max": int(done_in_window.max()), "used_for_ess": M},
+                                            "max": int(done_in_window.max()), "used_for_ess": int(Mk.sum()),
+                                            "used_equal_length": int(C * Mk.min())},
         "stepsize_per_chain": {"min": float(eps.min()), "median": float(np.median(eps)), "max": float(eps.max())},
         "leapfrogs_per_transition": float(nchains * K / max(1, done_in_window.sum())),
         "rows_x_chains_per_sec": grads * rows_per_shard / elapsed,

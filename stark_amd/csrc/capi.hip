@@ -24,7 +24,9 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
 bool stk_sweep_supported(int C, int d);
 hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, int nsh, int64_t n, int d, int T, int LD, int G,
                             int Gs, size_t lds, const double* q, int C, int Dp, double* partial, const int* req_step,
-                            int step_id, int* ran, hipStream_t st);
+                            int step_id, int* ran, hipStream_t st, const SweepWs* ws = nullptr);
+size_t stk_sweep_ws_bytes(int64_t n_max, int d, int C, int nshards);
+SweepWs stk_sweep_ws(void* base, int64_t n_max, int d, int nshards);
 hipError_t stk_launch_sweep_reduce(int family, const ShardDev* shards_dev, int shard0, int nsh, int d, int G, int Gs,
                                    const double* q, int C, int Dp, double* partial, const int* req_step, int step_id,
                                    double* lp_out, double* g_out, hipStream_t st);
@@ -124,7 +126,8 @@ struct stk_sampler {
   int64_t shard_sweeps = 0;
   double sweep_ms = 0.0;
   std::vector<DevBuf> bufs;
-  DevBuf partial, lp, g, ran;
+  DevBuf partial, lp, g, ran, ws;
+  SweepWs sws{};
   int Gs = 1;
   struct Group { int shard0, nsh, T, LD, G; size_t lds; };
   std::vector<Group> groups;
@@ -422,10 +425,17 @@ int stk_log_density_grad(stk_model* m, int shard, const double* q, int32_t C, do
   } else {
     int T, LD, G;
     size_t lds;
-    // the chain batch the sampler's sweep uses: 16 (fp64 MFMA) when 16 or more points are asked for
-    const int Cb = C <= 1 ? 1 : (C <= 2 ? 2 : (C < 16 || !stk_sweep_supported(16, s.d) ? 4 : 16));
+    // the chain batch the sampler's sweep uses: 64 (two-pass fp64 MFMA GEMMs) from 64 points,
+    // 16 (fp64 MFMA) from 16 when d <= 128, else 4 / 2 / 1
+    const int Cb = C <= 1 ? 1 : (C <= 2 ? 2 : (C >= 64 ? 64 : (C < 16 || !stk_sweep_supported(16, s.d) ? 4 : 16)));
     stk_sweep_geometry(s.n, s.d, &T, &LD, &G, &lds, Cb);
     const int PW = s.d + 2;
+    const size_t wsb = stk_sweep_ws_bytes(s.n, s.d, Cb, m->nshards);
+    SweepWs ws{};
+    if (wsb) {
+      RC(ctx->scratch[4].ensure(wsb));
+      ws = stk_sweep_ws(ctx->scratch[4].p, s.n, s.d, m->nshards);
+    }
     RC(ctx->scratch[0].ensure(sizeof(double) * (size_t)(m->nshards * Cb) * Dp));
     RC(ctx->scratch[1].ensure(sizeof(double) * (size_t)(m->nshards * Cb)));
     RC(ctx->scratch[2].ensure(sizeof(double) * (size_t)(m->nshards * Cb) * Dp));
@@ -439,7 +449,7 @@ int stk_log_density_grad(stk_model* m, int shard, const double* q, int32_t C, do
         STK_HIP_CHECK(hipMemcpyAsync(qb + (size_t)c * Dp, q + (size_t)src * D, sizeof(double) * D, hipMemcpyDefault, st));
       }
       STK_HIP_CHECK(stk_launch_sweep(m->family, shd, shard, 1, s.n, s.d, T, LD, G, G, lds, ctx->scratch[0].as<double>(), Cb,
-                                     Dp, ctx->scratch[3].as<double>(), nullptr, 0, nullptr, st));
+                                     Dp, ctx->scratch[3].as<double>(), nullptr, 0, nullptr, st, wsb ? &ws : nullptr));
       STK_HIP_CHECK(stk_launch_sweep_reduce(m->family, shd, shard, 1, s.d, G, G, ctx->scratch[0].as<double>(), Cb, Dp,
                                             ctx->scratch[3].as<double>(), nullptr, 0, ctx->scratch[1].as<double>(),
                                             ctx->scratch[2].as<double>(), st));
@@ -479,6 +489,7 @@ int stk_sampler_destroy(stk_sampler* s) {
   s->lp.release();
   s->g.release();
   s->ran.release();
+  s->ws.release();
   for (auto e : s->ev) hipEventDestroy(e);
   delete s;
   model_release(m);
@@ -497,7 +508,7 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   const int nch = stk_nch_for(m->Dmax);
   ARG_CHECK(nch > 0, "dimension %d too large (max 1024)", m->Dmax);
   if (m->family == STK_SCHOOLS) ARG_CHECK(nch <= 2, "8-schools supports J <= 126");
-  else ARG_CHECK(stk_sweep_supported(cfg->chains, m->d), "chains per shard must be 1, 2, 4, 8 or 16 (16: d <= 128) for regressions");
+  else ARG_CHECK(stk_sweep_supported(cfg->chains, m->d), "chains per shard must be 1, 2, 4, 8, 16 (d <= 128) or 64 for regressions");
   stk_sampler* s = new stk_sampler();
   s->m = m;
   m->refs++;
@@ -618,6 +629,13 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
     }
     s->Gs = gmax;
     rc = s->partial.ensure(sizeof(double) * (size_t)m->nshards * gmax * cfg->chains * (m->d + 2));
+    int64_t nmax = 0;
+    for (int sh = 0; sh < m->nshards; ++sh) nmax = std::max<int64_t>(nmax, m->sh[sh].n);
+    const size_t wsb = stk_sweep_ws_bytes(nmax, m->d, cfg->chains, m->nshards);
+    if (rc == STK_OK && wsb) {
+      rc = s->ws.ensure(wsb);
+      if (rc == STK_OK) s->sws = stk_sweep_ws(s->ws.p, nmax, m->d, m->nshards);
+    }
     if (rc == STK_OK) rc = s->ran.ensure(sizeof(int) * 64);
   }
   if (rc == STK_OK) {
@@ -677,7 +695,7 @@ static int run_split_batch(stk_sampler* s, int nsteps, int pause_at) {
     for (const auto& gr : s->groups) {
       STK_HIP_CHECK(stk_launch_sweep(m->family, A.shards, gr.shard0, gr.nsh, m->sh[gr.shard0].n, m->d, gr.T, gr.LD, gr.G, s->Gs, gr.lds,
                                      A.qeval, A.C, A.Dp, s->partial.as<double>(), A.req_step, step_id,
-                                     prof ? s->ran.as<int>() : nullptr, st));
+                                     prof ? s->ran.as<int>() : nullptr, st, s->sws.qT ? &s->sws : nullptr));
     }
     if (prof) STK_HIP_CHECK(hipEventRecord(s->ev[2 * k + 1], st));
     for (const auto& gr : s->groups) {

@@ -39,6 +39,13 @@ struct ShardDev {
   int P;                // output columns (params + transformed params + lp__)
 };
 
+// Workspace of the two-pass (v5, 64-chain) sweep: beta^T images and the residual matrix.
+struct SweepWs {
+  double* qT;       // [nshards][KP][64]
+  double* R;        // [nshards][Rrows][64]
+  int64_t Rrows;    // rows per shard, n rounded up to 64
+};
+
 // ---- per-chain NUTS state (global memory, one block of Dp-strided vectors per chain)
 enum Vec : int {
   V_Q, V_P, V_G,        // current integration point z (g = dV/dq = -grad lp)

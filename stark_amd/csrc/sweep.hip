@@ -36,6 +36,9 @@ struct SweepArgs {
   int shard0;             // first shard of this launch
   int Gs;                 // partial-buffer stride in chunks per shard (>= G)
   int* ran;               // optional: ran[step_id & 63] = 1 when any shard swept
+  double* qT;             // v5 workspace: [nshards][KP][64] swizzled beta^T images (KP = d rounded to 32)
+  double* R;              // v5 workspace: [nshards][Rrows][64] residuals d eta, swizzled rows
+  int64_t Rrows;          // v5: rows of R per shard (n rounded up to 64)
 };
 
 template <int FAM, int C, int T, int JPT, int VEC>
@@ -953,6 +956,264 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
   }
 }
 
+// v5 sweep: 64 chains of a shard, any d -- two fp64 MFMA GEMM passes (BASELINE configs[4]:
+// full-data logistic regression, d = 1000, 64 chains).
+//
+// At d*C = 64000 neither beta (B operand, d x 64) nor the gradient accumulators fit a
+// workgroup's registers, so the sweep is split at the residual:
+//   pass F  eta = X . [beta_1 .. beta_64] (M = rows, N = chains, K = d), + alpha, residual
+//           on the fly: d eta -> R (HBM, 512 B per row), lp and sum(d eta) per chain;
+//   pass B  G = X^T . R (M = d, N = chains, K = rows) per (row chunk, 64-column block).
+// X crosses HBM twice per leapfrog (8d B per row each pass) plus R (1 KB per row), against
+// 4*d*64 flop per row: 15 flop/B at d = 1000, above the fp64 balance point, so both passes
+// are fp64-MFMA bound.  Both are the same LDS-staged GEMM skeleton:
+// 4 waves, double-buffered 16 KB + 16 KB stages moved by `buffer_load_dwordx4 ... lds`, a
+// k-step = one A fragment read + four B fragment reads (chain tiles) + four independent
+// v_mfma_f64_16x16x4_f64.  LDS images are XOR-swizzled in 16-B pieces so every fragment
+// read is bank-conflict free: X in pass F by per-lane DMA source offsets, beta^T and R by
+// their writers (k_qt_swizzle, pass F's epilogue).
+constexpr int G5_C = 64;      // chains (4 MFMA N tiles)
+constexpr int G5_KC = 32;     // pass F: columns per stage
+constexpr int G5_TR = 64;     // pass F: rows per tile (16 per wave)
+constexpr int G5_JB = 64;     // pass B: columns per block (16 per wave)
+constexpr int G5_RB = 32;     // pass B: rows per stage
+constexpr int G5_STAGE = 32 * 1024;   // bytes per stage (A image + B image)
+
+__host__ __device__ inline int g5_kp(int d) { return (d + G5_KC - 1) / G5_KC * G5_KC; }
+// byte offset of element (row r, chain c) in a 512-B-row chain image (beta^T rows k, R rows r)
+__device__ __forceinline__ int g5_chain_off(int r, int c) { return r * 512 + ((((c >> 1) ^ ((r & 1) << 3))) << 4) + ((c & 1) << 3); }
+
+// beta^T images for pass F: qT[shard][k][.] = beta_c[k] (0 for k >= d), swizzled as g5_chain_off.
+__global__ __launch_bounds__(256) void k_qt_swizzle(SweepArgs A, int d) {
+  const int shard = A.shard0 + blockIdx.y;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  const int KP = g5_kp(d);
+  const int i = blockIdx.x * 256 + threadIdx.x;     // k * 64 + c
+  if (i >= KP * G5_C) return;
+  const int k = i >> 6, c = i & 63;
+  const double v = k < d ? A.q[((size_t)shard * G5_C + c) * A.Dp + 1 + k] : 0.0;
+  char* img = reinterpret_cast<char*>(A.qT + (size_t)shard * KP * G5_C);
+  *reinterpret_cast<double*>(img + g5_chain_off(k, c)) = v;
+}
+
+// Pass F: one block per (shard, chunk); the chunk's 64-row tiles one after another.
+template <int FAM>
+__global__ __launch_bounds__(256, 2) void k_gemm_fwd(SweepArgs A) {
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d, KP = g5_kp(d), NKC = KP / G5_KC;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * G5_TR, r1 = std::min<int64_t>(sh.n, t1 * G5_TR);
+  const int nrows = (int)(r1 - r0);
+  const int ntile = (int)(t1 - t0);
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const stg = reinterpret_cast<char*>(lds);                 // 2 stages: [X 16 KB][beta^T 16 KB]
+  double* const sptab = reinterpret_cast<double*>(stg + 2 * G5_STAGE);
+  if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
+
+  // per-lane chain constants: chain 16 ct + lr
+  const double* qb = A.q + (size_t)shard * G5_C * A.Dp;
+  double alpha[4], inv_s[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    alpha[ct] = qb[(size_t)(16 * ct + lr) * A.Dp];
+    inv_s[ct] = (FAM == STK_LINREG) ? exp(-qb[(size_t)(16 * ct + lr) * A.Dp + d + 1]) : 0.0;
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0xF70);
+
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
+  const __amdgpu_buffer_rsrc_t br = uniform_rsrc(A.qT + (size_t)shard * KP * G5_C, (int64_t)KP * G5_C * 8);
+  // X stage: slot s (16 B) = row s>>4, piece (s & 15) ^ (row & 15) of the stage's 32 columns
+  int xvo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int sl = (w * 4 + i) * 64 + lane, row = sl >> 4, pc = (sl & 15) ^ (row & 15);
+    xvo[i] = row * d * 8 + pc * 16;
+  }
+  auto issue = [&](int st) {          // global stage index st = tile * NKC + kc
+    const int tile = st / NKC, kc = st % NKC;
+    char* b = stg + (st & 1) * G5_STAGE;
+    const int xso = tile * G5_TR * d * 8 + kc * G5_KC * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * 4 + i) * 1024), 16, xvo[i], xso, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(br, (lds_vptr)(b + 16384 + (w * 4 + i) * 1024), 16, lane * 16,
+                                               kc * G5_KC * 512 + (w * 4 + i) * 1024, 0, 0);
+  };
+
+  double lpa[4] = {0.0, 0.0, 0.0, 0.0}, gaa[4] = {0.0, 0.0, 0.0, 0.0};
+  char* const Rimg = reinterpret_cast<char*>(A.R + ((size_t)shard * A.Rrows + r0) * G5_C);
+  const int nst = ntile * NKC;
+  if (nst > 0) issue(0);
+  dbl4 acc[4];
+  for (int st = 0; st < nst; ++st) {
+    const int kc = st % NKC;
+    if (kc == 0) {
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) acc[ct] = dbl4{0.0, 0.0, 0.0, 0.0};
+    }
+    if (st + 1 < nst) { issue(st + 1); wait_vm<8>(); } else { wait_vm<0>(); }
+    __syncthreads();                                     // stage st landed for every wave
+    const char* b = stg + (st & 1) * G5_STAGE;
+    const int r = 16 * w + lr;
+#pragma unroll
+    for (int step = 0; step < G5_KC / 4; ++step) {
+      const int kk = 4 * step + lh;
+      const double a = *reinterpret_cast<const double*>(b + r * 256 + ((((kk >> 1) ^ (r & 15))) << 4) + ((kk & 1) << 3));
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+        acc[ct] = mfma_f64(a, *reinterpret_cast<const double*>(b + 16384 + g5_chain_off(kk, 16 * ct + lr)), acc[ct]);
+    }
+    __syncthreads();                                     // reads of this stage done before it is refilled
+    if (kc == NKC - 1) {                                 // ---- tile epilogue: residual, R, lp
+      // eta goes through this wave's own 8 KB of the stage just consumed (its DMA slots, which
+      // it refills only after this loop), so the 16 residuals run one at a time from LDS
+      // instead of holding 16 softplus evaluations' temporaries in registers
+      const int tile = st / NKC;
+      char* const b2 = stg + (st & 1) * G5_STAGE;
+      auto eslot = [&](int e) -> double* {
+        return reinterpret_cast<double*>(b2 + (e < 8 ? w * 4096 : 16384 + w * 4096) + (e & 7) * 512) + lane;
+      };
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *eslot(ct * 4 + i) = acc[ct][i];
+#pragma unroll 1
+      for (int e = 0; e < 16; ++e) {
+        const int ct = e >> 2, i = e & 3;
+        const int row = 16 * w + lh + 4 * i;               // row of the tile
+        const int64_t grow = (int64_t)tile * G5_TR + row;  // row of the chunk
+        const bool valid = grow < nrows;
+        double yv = 0.0;
+        if (valid) yv = (FAM == STK_LOGREG) ? (double)sh.yi[r0 + grow] : sh.y[r0 + grow];
+        const double al = ct == 0 ? alpha[0] : (ct == 1 ? alpha[1] : (ct == 2 ? alpha[2] : alpha[3]));
+        const double eta = *eslot(e) + al;
+        double dv, lt;
+        if constexpr (FAM == STK_LOGREG) {
+          const double sgn = 2.0 * yv - 1.0, ntt = sgn * eta;
+          double ex, lm, wt;
+          softplus_tab(ntt, sptab, &ex, &lm, &wt);
+          const bool hi = ntt > 20.0, lo = ntt < -20.0;
+          lt = hi ? -ex : (lo ? ntt : -lm);
+          dv = sgn * (hi ? ex : (lo ? 1.0 : wt));
+        } else {
+          const double is = ct == 0 ? inv_s[0] : (ct == 1 ? inv_s[1] : (ct == 2 ? inv_s[2] : inv_s[3]));
+          const double z = (yv - eta) * is;
+          lt = z * z;
+          dv = z * is;
+        }
+        dv = valid ? dv : 0.0;
+        lt = valid ? lt : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          lpa[q] += q == ct ? lt : 0.0;
+          gaa[q] += q == ct ? dv : 0.0;
+        }
+        *reinterpret_cast<double*>(Rimg + g5_chain_off((int)grow, 16 * ct + lr)) = dv;
+      }
+      __builtin_amdgcn_s_waitcnt(0xF70);                  // vmcnt(0): R stores retired before the next counted DMA wait
+    }
+  }
+
+  // ---- lp and sum(d eta) per chain: lanes lr of the 4 row groups of the 4 waves, fixed order
+  __syncthreads();
+  double* red = lds;                                     // [4 waves][64 lanes][4 ct][2]
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    red[((w * 64 + lane) * 4 + ct) * 2 + 0] = lpa[ct];
+    red[((w * 64 + lane) * 4 + ct) * 2 + 1] = gaa[ct];
+  }
+  __syncthreads();
+  if (tid < 2 * G5_C) {
+    const int c = tid >> 1, kind = tid & 1, ct = c >> 4, l = c & 15;
+    double v = 0.0;
+    for (int ww = 0; ww < 4; ++ww)
+      for (int h = 0; h < 4; ++h) v += red[((ww * 64 + h * 16 + l) * 4 + ct) * 2 + kind];
+    A.partial[(((size_t)shard * A.Gs + chunk) * G5_C + c) * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
+}
+
+// Pass B: one block per (shard, chunk, 64-column block); G[j][c] += X[r][j] R[r][c] over the
+// chunk's rows, straight into the chunk's partial row (columns 1 .. d).
+__global__ __launch_bounds__(256, 2) void k_gemm_bwd(SweepArgs A, int njb) {
+  const int jb = blockIdx.x % njb;
+  const int sc = blockIdx.x / njb;
+  const int shard = A.shard0 + sc / A.G;
+  const int chunk = sc % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * G5_TR, r1 = std::min<int64_t>(sh.n, t1 * G5_TR);
+  const int nrows = (int)(r1 - r0);
+  const int nst = (nrows + G5_RB - 1) / G5_RB;
+  const int j0 = jb * G5_JB;
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const stg = reinterpret_cast<char*>(lds);      // 2 stages: [X^T block 16 KB][R block 16 KB]
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
+  const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(A.R + ((size_t)shard * A.Rrows + r0) * G5_C, (int64_t)nrows * G5_C * 8);
+  // X stage: slot s = row s >> 5, piece (s & 31) ^ ((row & 1) << 3) of the block's 64 columns
+  int xvo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int sl = (w * 4 + i) * 64 + lane, row = sl >> 5, pc = (sl & 31) ^ ((row & 1) << 3);
+    xvo[i] = row * d * 8 + (j0 + 2 * pc) * 8;
+  }
+  auto issue = [&](int st) {
+    char* b = stg + (st & 1) * G5_STAGE;
+    const int xso = st * G5_RB * d * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * 4 + i) * 1024), 16, xvo[i], xso, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (lds_vptr)(b + 16384 + (w * 4 + i) * 1024), 16, lane * 16,
+                                               st * G5_RB * 512 + (w * 4 + i) * 1024, 0, 0);
+  };
+  dbl4 acc[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) acc[ct] = dbl4{0.0, 0.0, 0.0, 0.0};
+  if (nst > 0) issue(0);
+  const int jl = 16 * w + lr;                          // A row (column of X) of this lane
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) { issue(st + 1); wait_vm<8>(); } else { wait_vm<0>(); }
+    __syncthreads();
+    const char* b = stg + (st & 1) * G5_STAGE;
+#pragma unroll
+    for (int step = 0; step < G5_RB / 4; ++step) {
+      const int r = 4 * step + lh;
+      const double a = *reinterpret_cast<const double*>(b + r * 512 + ((((jl >> 1) ^ ((r & 1) << 3))) << 4) + ((jl & 1) << 3));
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+        acc[ct] = mfma_f64(a, *reinterpret_cast<const double*>(b + 16384 + g5_chain_off(r, 16 * ct + lr)), acc[ct]);
+    }
+    __syncthreads();
+  }
+  double* out = A.partial + ((size_t)shard * A.Gs + chunk) * G5_C * A.PW;
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = j0 + 16 * w + lh + 4 * i;
+      if (j < d) out[(size_t)(16 * ct + lr) * A.PW + 1 + j] = acc[ct][i];
+    }
+  }
+}
+
 // Sum chunk partials in chunk order and finish the family's lp / gradient.
 // grid (nshards*C, ceil(PW/64)), 256 threads: 4 waves split the chunks, fixed combine order.
 template <int FAM>
@@ -1034,6 +1295,7 @@ static int sweepm_nb(int d, int minb = SM_MINB) {
 }
 
 static int sweep_variant(int64_t n, int d, int C) {
+  if (C == G5_C) return (((n + 511) / 512 + G5_TR) * d * 8 < ((int64_t)1 << 31)) ? 5 : 0;   // chunk bytes fit a buffer descriptor
   if (C == SM_C) return (d <= 128 && sweepm_nb(d) >= 1 && (n * d * 8) / 512 < ((int64_t)1 << 30)) ? 4 : 0;
   const int f = sweep_forced();
   const bool v3ok = d % 2 == 0 && d / 2 <= S3_KMAX && (C == 1 || C == 2 || C == 4) && sweep3_nb(d, C) >= 3 &&
@@ -1047,6 +1309,17 @@ static int sweep_variant(int64_t n, int d, int C) {
 
 void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_bytes, int C) {
   const int var = sweep_variant(n, d, C);
+  if (var == 5) {
+    const int64_t nt = (n + G5_TR - 1) / G5_TR;
+    int64_t g = (nt + 3) / 4;            // >= 4 tiles of 64 rows per chunk
+    if (g > 512) g = 512;
+    if (g < 1) g = 1;
+    *T = G5_TR;
+    *LD = 0;
+    *G = (int)g;
+    *lds_bytes = 2 * G5_STAGE + SP_TAB * sizeof(double);
+    return;
+  }
   if (var == 4) {
     const int64_t nt = (n + 63) / 64;
     int64_t g = (nt + 7) / 8;            // >= 8 tiles of 64 rows per chunk (as v3)
@@ -1188,17 +1461,46 @@ static hipError_t pick_c(const SweepArgs& A, int64_t n, int d, int T, int nblock
 }
 
 bool stk_sweep_supported(int C, int d) {
+  if (C == G5_C) return d >= 1 && d <= 4096;
   if (C == SM_C) return d >= 1 && d <= 128;
   if (!(C == 1 || C == 2 || C == 4 || C == 8)) return false;
   return d >= 1 && d <= 1024;
 }
 
+// Workspace bytes of the sweep for `nshards` shards of at most n_max rows (0 unless v5).
+size_t stk_sweep_ws_bytes(int64_t n_max, int d, int C, int nshards) {
+  if (sweep_variant(n_max, d, C) != 5) return 0;
+  const int64_t rrows = (n_max + G5_TR - 1) / G5_TR * G5_TR;
+  return sizeof(double) * (size_t)nshards * G5_C * ((size_t)g5_kp(d) + (size_t)rrows);
+}
+SweepWs stk_sweep_ws(void* base, int64_t n_max, int d, int nshards) {
+  SweepWs w{};
+  w.Rrows = (n_max + G5_TR - 1) / G5_TR * G5_TR;
+  w.qT = reinterpret_cast<double*>(base);
+  w.R = w.qT + (size_t)nshards * g5_kp(d) * G5_C;
+  return w;
+}
+
 // Launch the sweep over `nsh` shards starting at shard0 (all with the same n, d geometry).
 hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, int nsh, int64_t n, int d, int T,
                             int LD, int G, int Gs, size_t lds, const double* q, int C, int Dp, double* partial,
-                            const int* req_step, int step_id, int* ran, hipStream_t st) {
+                            const int* req_step, int step_id, int* ran, hipStream_t st, const SweepWs* ws = nullptr) {
   SweepArgs A{shards_dev, q, partial, req_step, step_id, C, Dp, G, LD, d + 2, shard0, Gs, ran};
   const int nblocks = nsh * G;
+  if (sweep_variant(n, d, C) == 5) {
+    if (!ws || !ws->qT || !ws->R || ws->Rrows < (n + G5_TR - 1) / G5_TR * G5_TR) return hipErrorInvalidValue;
+    A.qT = ws->qT;
+    A.R = ws->R;
+    A.Rrows = ws->Rrows;
+    const int njb = (d + G5_JB - 1) / G5_JB;
+    hipLaunchKernelGGL(k_qt_swizzle, dim3((g5_kp(d) * G5_C + 255) / 256, nsh), dim3(256), 0, st, A, d);
+    auto kf = family == STK_LOGREG ? k_gemm_fwd<STK_LOGREG> : k_gemm_fwd<STK_LINREG>;
+    allow_big_lds((const void*)kf);
+    hipLaunchKernelGGL(kf, dim3(nblocks), dim3(256), lds, st, A);
+    allow_big_lds((const void*)k_gemm_bwd);
+    hipLaunchKernelGGL(k_gemm_bwd, dim3(nblocks * njb), dim3(256), 2 * G5_STAGE, st, A, njb);
+    return hipGetLastError();
+  }
   if (family == STK_LOGREG) return pick_c<STK_LOGREG>(A, n, d, T, nblocks, lds, st);
   if (family == STK_LINREG) return pick_c<STK_LINREG>(A, n, d, T, nblocks, lds, st);
   return hipErrorInvalidValue;

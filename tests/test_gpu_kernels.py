@@ -31,14 +31,17 @@ def test_schools_lpgrad(ctx, orc):
 
 
 # shapes cover every sweep variant: v3 LDS-DMA ring (even d <= 104: partial last tile, one tile,
-# many chunks, d = 2), v2 (even d <= 128 beyond v3), v1 (odd or wide d), v4 (C = 16, d <= 128)
+# many chunks, d = 2), v2 (even d <= 128 beyond v3), v1 (odd or wide d), v4 (C = 16, d <= 128), v5 (C = 64, any d)
 @pytest.mark.parametrize("n,d,C", [(1, 1, 5), (7, 3, 5), (1000, 100, 5), (4097, 50, 5), (333, 129, 5),
                                    (257, 300, 5), (100, 700, 5), (5000, 2, 5), (64, 65, 5), (64, 100, 5),
                                    (65, 104, 3), (20000, 100, 4), (3000, 120, 5), (1000, 100, 1), (777, 100, 2),
                                    # v4 fp64 MFMA (16 chains per launch; 20 = two batches, the second padded)
                                    (1, 1, 16), (7, 3, 16), (1000, 100, 16), (4097, 50, 16), (333, 128, 16),
                                    (65, 104, 20), (20000, 100, 16), (64, 65, 16), (5000, 2, 16), (129, 17, 16),
-                                   (333, 129, 16)])
+                                   (333, 129, 16),
+                                   # v5 two-pass fp64 MFMA GEMMs (64 chains; 70 = two batches)
+                                   (1, 1, 64), (7, 3, 64), (4097, 50, 64), (333, 129, 64), (257, 300, 64),
+                                   (1000, 1000, 64), (130, 1001, 70), (5000, 100, 64)])
 @pytest.mark.parametrize("family", ["logistic", "linear"])
 def test_regression_lpgrad(ctx, orc, family, n, d, C):
     from stark_amd import engine

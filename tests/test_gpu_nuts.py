@@ -122,7 +122,7 @@ def test_schools_4096_chains_exact_moments(ctx, orc):
     s.close()
 
 
-@pytest.mark.parametrize("C", [8, 16])      # 16: the fp64 MFMA sweep (v4)
+@pytest.mark.parametrize("C", [8, 16, 64])      # 16: the fp64 MFMA sweep (v4); 64: two-pass GEMMs (v5)
 def test_linear_regression_closed_form(ctx, orc, C):
     from stark_amd import engine
     rng = np.random.default_rng(8)
@@ -143,7 +143,7 @@ def test_linear_regression_closed_form(ctx, orc, C):
     s.close()
 
 
-@pytest.mark.parametrize("C", [8, 16])
+@pytest.mark.parametrize("C", [8, 16, 64])
 def test_logistic_matches_oracle_moments(ctx, orc, C):
     from stark_amd import engine
     rng = np.random.default_rng(12)
@@ -185,7 +185,7 @@ def test_bitwise_reproducible_and_resumable(ctx, C):
     b.close()
 
 
-@pytest.mark.parametrize("C", [4, 16])
+@pytest.mark.parametrize("C", [4, 16, 64])
 def test_shard_placement_independent(ctx, C):
     """1 GPU holding 4 shards == 4 GPUs holding one shard each (same global shard ids)."""
     from stark_amd import engine

@@ -190,6 +190,14 @@ int main(int argc, char** argv) {
   size_t lds;
   stk_sweep_geometry(rows, d, &T, &LD, &G, &lds, C);
   CK(hipMalloc(&partial, sizeof(double) * (size_t)nsh * G * C * (d + 2)));
+  const size_t wsb = stk_sweep_ws_bytes(rows, d, C, nsh);
+  SweepWs ws{};
+  if (wsb) {
+    void* wp;
+    CK(hipMalloc(&wp, wsb));
+    ws = stk_sweep_ws(wp, rows, d, nsh);
+  }
+  const SweepWs* wsp = wsb ? &ws : nullptr;
   CK(hipMalloc(&lp, sizeof(double) * nsh * C));
   CK(hipMalloc(&grad, sizeof(double) * nsh * C * Dp));
   CK(hipMalloc(&sink, sizeof(double) * nsh * G));
@@ -217,9 +225,10 @@ int main(int argc, char** argv) {
   });
   SweepArgs A{sh_d, q, partial, nullptr, 0, C, Dp, G, d | 1, d + 2, 0, G, nullptr};
   hipFuncSetAttribute((const void*)k_skeleton<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  timeit("skeleton", (double)nsh * rows * 8.0 * d, [&] {   // v2's register pipeline, no arithmetic
-    hipLaunchKernelGGL(k_skeleton<64>, dim3(nsh * G), dim3(256), (size_t)64 * (d | 1) * 8, st, A, sink);
-  });
+  if ((size_t)64 * (d | 1) * 8 <= 160 * 1024)
+    timeit("skeleton", (double)nsh * rows * 8.0 * d, [&] {   // v2's register pipeline, no arithmetic
+      hipLaunchKernelGGL(k_skeleton<64>, dim3(nsh * G), dim3(256), (size_t)64 * (d | 1) * 8, st, A, sink);
+    });
   {
     const int K = d / 2;
     for (int nb = 2; nb <= 6; ++nb) {
@@ -271,7 +280,7 @@ int main(int argc, char** argv) {
     abl("v4 -all", k_sweepm<STK_LOGREG, 25, 7, 7>);
     const double fl = 4.0 * d * C * (double)rows * nsh;   // algorithmic fp64 flops of one sweep
     timeit("v4 flops", fl, [&] {
-      CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st));
+      CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st, wsp));
     });
     printf("  (v4 flops line: 'GB/s' column = GFLOP/s of the sweep's 4*d*C flop per row)\n");
     for (int wpb = 1; wpb <= 4; wpb *= 2) {
@@ -283,11 +292,18 @@ int main(int argc, char** argv) {
       });
     }
   }
+  if (sweep_variant(rows, d, C) == 5) {
+    const double fl = 4.0 * d * C * (double)rows * nsh;
+    timeit("v5 flops", fl, [&] {
+      CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st, wsp));
+    });
+    printf("  (v5 flops line: 'GB/s' column = GFLOP/s of the two GEMMs, 4*d*C flop per row)\n");
+  }
   timeit("sweep", bytes, [&] {
-    CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st));
+    CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st, wsp));
   });
   timeit("sweep+red", bytes, [&] {
-    CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st));
+    CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st, wsp));
     CK(stk_launch_sweep_reduce(STK_LOGREG, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
   });
   CK(hipStreamSynchronize(st));
