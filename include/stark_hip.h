@@ -120,6 +120,11 @@ STK_API void stk_config_default(stk_config* cfg);
 STK_API int stk_ctx_create(int device, stk_ctx** out);
 STK_API int stk_ctx_destroy(stk_ctx* ctx);
 STK_API int stk_ctx_sync(stk_ctx* ctx);
+/* A context on the caller's HIP stream (e.g. torch.cuda.current_stream().cuda_stream), so library
+ * kernels and the caller's collectives on that stream are ordered without host syncs (NULL: the
+ * null stream, which is torch's default current stream).  The stream is not destroyed with the
+ * context. */
+STK_API int stk_ctx_create_on_stream(int device, void* stream, stk_ctx** out);
 STK_API int stk_ctx_set_profiling(stk_ctx* ctx, int on);   /* HIP events around sweeps */
 STK_API void* stk_ctx_stream(stk_ctx* ctx);                /* hipStream_t of the context */
 
@@ -157,6 +162,21 @@ STK_API int stk_sampler_adaptation(stk_sampler* s, double* stepsize, double* inv
 /* Transitions completed so far by every chain (nshards * chains, shard-major). */
 STK_API int stk_sampler_iterations(stk_sampler* s, int32_t* iters);
 STK_API int stk_sampler_destroy(stk_sampler* s);
+
+/* ---- full-data mode (BASELINE configs[4]): ONE posterior whose rows are split over ranks.
+ * Every rank builds a one-shard model of its rows and a sampler with the same config and the
+ * same shard_ids (so the chains' RNG streams agree); after each step's local sweep + reduce,
+ * `fn` must replace the [nchains][Dp] gradient block followed by the [nchains] log densities
+ * (count = nchains * (Dp + 1) doubles, stk_sampler_grad_block) by their sum over ranks, ordered
+ * on `stream` (the context's stream), and return 0.  Every rank then runs the NUTS step on
+ * identical inputs, so chain states stay identical without any other exchange.  dev_block:
+ * NULL (the library's block), or caller-allocated device memory of `count` doubles used in
+ * its place -- e.g. a torch tensor that torch.distributed.all_reduce sums over RCCL.  Logistic
+ * family only (its log density is a pure sum over rows); call before the first run.
+ * No reference counterpart (SURVEY.md 8e "full-data extension"). */
+typedef int (*stk_allreduce_fn)(void* user, double* block, int64_t count, void* stream);
+STK_API int stk_sampler_grad_block(stk_sampler* s, int64_t* count);
+STK_API int stk_sampler_set_allreduce(stk_sampler* s, stk_allreduce_fn fn, void* user, double* dev_block);
 STK_API int stk_sample(stk_model* m, const stk_config* cfg, double* draws, double* stats, stk_run_info* info);
 
 /* One fixed-step-size NUTS transition per chain from q (C x D, updated in place), no

@@ -68,6 +68,7 @@ SIGNATURES = [
     ("stk_version", ctypes.c_int, []),
     ("stk_config_default", None, [ctypes.POINTER(Config)]),
     ("stk_ctx_create", ctypes.c_int, [ctypes.c_int, _pp]),
+    ("stk_ctx_create_on_stream", ctypes.c_int, [ctypes.c_int, _vp, _pp]),
     ("stk_ctx_destroy", ctypes.c_int, [_vp]),
     ("stk_ctx_sync", ctypes.c_int, [_vp]),
     ("stk_ctx_set_profiling", ctypes.c_int, [_vp, ctypes.c_int]),
@@ -90,12 +91,17 @@ SIGNATURES = [
     ("stk_sampler_adaptation", ctypes.c_int, [_vp, _vp, _vp]),
     ("stk_sampler_iterations", ctypes.c_int, [_vp, _vp]),
     ("stk_sampler_destroy", ctypes.c_int, [_vp]),
+    ("stk_sampler_grad_block", ctypes.c_int, [_vp, ctypes.POINTER(_i64)]),
+    ("stk_sampler_set_allreduce", ctypes.c_int, [_vp, _vp, _vp, _vp]),
     ("stk_sample", ctypes.c_int, [_vp, ctypes.POINTER(Config), _vp, _vp, ctypes.POINTER(RunInfo)]),
     ("stk_transition", ctypes.c_int, [_vp, ctypes.c_int, _vp, _i32, _u64, _i32, _dbl, _vp, _i32, _vp, _vp]),
     ("stk_consensus_products", ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
     ("stk_consensus_solve", ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _vp]),
     ("stk_consensus", ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
 ]
+
+# int (*stk_allreduce_fn)(void* user, double* block, int64_t count, void* stream)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 
 _lib = None
 

@@ -97,6 +97,7 @@ struct DevBuf {
 struct stk_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  bool own_stream = true;     // false: a caller's stream (stk_ctx_create_on_stream), not destroyed here
   int profiling = 0;
   int refs = 1;
   DevBuf scratch[8];
@@ -128,6 +129,8 @@ struct stk_sampler {
   std::vector<DevBuf> bufs;
   DevBuf partial, lp, g, ran, ws;
   SweepWs sws{};
+  stk_allreduce_fn ar_fn = nullptr;   // full-data mode: rank-sum of [grad | lp] after every reduce
+  void* ar_user = nullptr;
   int Gs = 1;
   struct Group { int shard0, nsh, T, LD, G; size_t lds; };
   std::vector<Group> groups;
@@ -179,12 +182,26 @@ int stk_ctx_create(int device, stk_ctx** out) {
   return STK_OK;
 }
 
+int stk_ctx_create_on_stream(int device, void* stream, stk_ctx** out) {
+  ARG_CHECK(out, "stk_ctx_create_on_stream: out is NULL");   // stream NULL = the device's null stream
+  int n = 0;
+  STK_HIP_CHECK(hipGetDeviceCount(&n));
+  ARG_CHECK(device >= 0 && device < n, "stk_ctx_create_on_stream: device %d not in [0, %d)", device, n);
+  STK_HIP_CHECK(hipSetDevice(device));
+  stk_ctx* c = new stk_ctx();
+  c->device = device;
+  c->stream = (hipStream_t)stream;
+  c->own_stream = false;
+  *out = c;
+  return STK_OK;
+}
+
 static void ctx_release(stk_ctx* c) {
   if (--c->refs > 0) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   for (auto& b : c->scratch) b.release();
-  hipStreamDestroy(c->stream);
+  if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -559,8 +576,9 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   ALLOC(iv, int, (size_t)nchains * I_COUNT);
   ALLOC(cnt, unsigned long long, (size_t)nchains * C_COUNT);
   ALLOC(qeval, double, (size_t)nchains * Dp);
-  ALLOC(lp_in, double, (size_t)nchains);
-  ALLOC(g_in, double, (size_t)nchains * Dp);
+  // g_in and lp_in are one block, [nchains][Dp] then [nchains]: the unit of the full-data all-reduce
+  ALLOC(g_in, double, (size_t)nchains * Dp + nchains);
+  if (rc == STK_OK) A.lp_in = A.g_in + (size_t)nchains * Dp;
   ALLOC(draws, double, (size_t)m->nshards * m->Pmax * A.S_total);
   ALLOC(stats, double, (size_t)m->nshards * A.S_total * N_STATS);
   A.ud_first = cfg->save_warmup ? 0 : cfg->num_warmup;
@@ -702,6 +720,13 @@ static int run_split_batch(stk_sampler* s, int nsteps, int pause_at) {
       STK_HIP_CHECK(stk_launch_sweep_reduce(m->family, A.shards, gr.shard0, gr.nsh, m->d, gr.G, s->Gs, A.qeval, A.C,
                                             A.Dp, s->partial.as<double>(), A.req_step, step_id, A.lp_in, A.g_in, st));
     }
+    if (s->ar_fn) {
+      const int r = s->ar_fn(s->ar_user, A.g_in, (int64_t)A.nchains * (A.Dp + 1), (void*)st);
+      if (r != 0) {
+        stk_set_error("full-data all-reduce callback failed (%d) at step %d", r, step_id);
+        return STK_E_STATE;
+      }
+    }
     STK_HIP_CHECK(stk_launch_nuts_step(A, s->nch, step_id, pause_at, st));
     s->step++;
     s->steps++;
@@ -748,6 +773,29 @@ int stk_sampler_run(stk_sampler* s, int32_t target_iter, int64_t max_steps) {
     }
   }
   STK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  return STK_OK;
+}
+
+int stk_sampler_grad_block(stk_sampler* s, int64_t* count) {
+  ARG_CHECK(s && count, "stk_sampler_grad_block: bad arguments");
+  *count = (int64_t)s->A.nchains * (s->A.Dp + 1);
+  return STK_OK;
+}
+
+int stk_sampler_set_allreduce(stk_sampler* s, stk_allreduce_fn fn, void* user, double* dev_block) {
+  ARG_CHECK(s, "stk_sampler_set_allreduce: NULL sampler");
+  ARG_CHECK(s->m->family == STK_LOGREG,
+            "full-data mode needs a purely additive log density (logistic: flat priors, no Jacobian term)");
+  ARG_CHECK(s->step == 0, "stk_sampler_set_allreduce: call before the first stk_sampler_run");
+  const size_t n = (size_t)s->A.nchains * (s->A.Dp + 1);
+  if (dev_block) {
+    STK_HIP_CHECK(hipSetDevice(s->m->ctx->device));
+    STK_HIP_CHECK(hipMemsetAsync(dev_block, 0, sizeof(double) * n, s->m->ctx->stream));
+    s->A.g_in = dev_block;
+    s->A.lp_in = dev_block + (size_t)s->A.nchains * s->A.Dp;
+  }
+  s->ar_fn = fn;
+  s->ar_user = user;
   return STK_OK;
 }
 

@@ -56,10 +56,16 @@ def _ptr(a):
 class Context:
     """One device + one HIP stream (``stk_ctx``)."""
 
-    def __init__(self, device: int = 0, profiling: bool = False):
+    def __init__(self, device: int = 0, profiling: bool = False, stream: int | None = None):
+        """stream: None (the context's own HIP stream) or a caller's hipStream_t handle, e.g.
+        ``torch.cuda.current_stream(device).cuda_stream``, so the library's kernels and the
+        caller's torch.distributed collectives are ordered on one stream (full-data mode)."""
         lib = _lib.load()
         h = ctypes.c_void_p()
-        check(lib.stk_ctx_create(int(device), ctypes.byref(h)))
+        if stream is None:
+            check(lib.stk_ctx_create(int(device), ctypes.byref(h)))
+        else:
+            check(lib.stk_ctx_create_on_stream(int(device), ctypes.c_void_p(int(stream)), ctypes.byref(h)))
         self._h = h
         self.device = device
         _live["ctx"].add(self)
@@ -301,6 +307,27 @@ class Sampler:
         """Advance every chain to `target_iter` completed transitions (default: all)."""
         t = self.total if target_iter is None else int(target_iter)
         check(_lib.load().stk_sampler_run(self._h, t, int(max_steps)))
+        return self
+
+    def grad_block(self) -> int:
+        """Doubles in the per-step [grad | lp] block that full-data mode sums over ranks."""
+        n = ctypes.c_int64()
+        check(_lib.load().stk_sampler_grad_block(self._h, ctypes.byref(n)))
+        return int(n.value)
+
+    def set_allreduce(self, fn, block_ptr: int | None = None):
+        """Full-data mode: fn(block_ptr, count, stream) -> None is called after every step's
+        local sweep + reduce and must leave the sum over ranks in the block (stk_sampler_set_allreduce)."""
+        def _cb(user, ptr, count, stream):
+            try:
+                fn(ptr, count, stream)
+                return 0
+            except Exception as e:   # reported through the library's error path
+                self._cb_error = e
+                return -1
+        self._cb = _lib.ALLREDUCE_FN(_cb)            # keep the trampoline alive with the sampler
+        check(_lib.load().stk_sampler_set_allreduce(self._h, self._cb, None,
+                                                    ctypes.c_void_p(block_ptr) if block_ptr else None))
         return self
 
     def info(self) -> dict:

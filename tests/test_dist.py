@@ -69,3 +69,58 @@ def test_gloo_world2_gather_and_driver(golden):
     st = _fake_stark(mpatch)
     np.testing.assert_array_equal(st.distribute(n=3, iter=100, reference_union=True), res[0][3])
     mpatch.undo()
+
+
+# ---------------------------------------------------------------- full-data mode exchange
+def _fulldata_worker(rank, world, port, q):
+    """Each rank: oracle lp/grad of ITS rows (fulldata.rank_rows) in the library's block layout
+    ([C][Dp] gradients, then [C] log densities), summed by fulldata.sum_over_ranks -- the
+    exchange the GPU path runs after every step -- must equal the full-data oracle."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from stark_amd import fulldata
+        O.build()
+        n, d, C = 1001, 7, 3
+        Dp = (d + 1 + 7) // 8 * 8
+        X = O.gen_x(5, 0, n, d)
+        beta = O.gen_beta(5, d)
+        y, _ = O.gen_y_logistic(5, 0, X, 0.0, beta)
+        q_ = np.random.default_rng(3).normal(0, 0.3, (C, d + 1))
+        off, cnt = fulldata.rank_rows(n, world, rank)
+        om = O.Model(O.FAM_LOGREG, X=X[off:off + cnt], y=y[off:off + cnt])
+        block = torch.zeros(C * Dp + C, dtype=torch.float64)
+        for c in range(C):
+            lp, g = om.lpgrad(q_[c])
+            block[c * Dp:c * Dp + d + 1] = torch.from_numpy(g)
+            block[C * Dp + c] = lp
+        fulldata.sum_over_ranks(block)
+        full = O.Model(O.FAM_LOGREG, X=X, y=y)
+        ok = True
+        for c in range(C):
+            lp, g = full.lpgrad(q_[c])
+            ok &= abs(block[C * Dp + c].item() - lp) <= 1e-12 * abs(lp)
+            ok &= bool(np.allclose(block[c * Dp:c * Dp + d + 1].numpy(), g, rtol=1e-12, atol=1e-12 * np.abs(g).max()))
+        q.put((rank, ok, (off, cnt)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_fulldata_exchange():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fulldata_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] for r in res)
+    assert res[0][2] == (0, 500) and res[1][2] == (500, 501)

@@ -1,5 +1,7 @@
 """GPU NUTS (iterative per-chain state machine) vs the oracle's recursive Stan 2.19 twin,
 exact posterior moments, and reproducibility across runs / shard placements."""
+import os
+
 import numpy as np
 import pytest
 
@@ -228,3 +230,37 @@ def test_driver_weighted_matches_reference(ctx, golden, monkeypatch):
     out = st.concensusWeight(iter=600)
     ref = g["weighted"]
     np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-10 * np.abs(ref).max())
+
+
+# ---------------------------------------------------------------- full-data mode (configs[4])
+@pytest.mark.parametrize("C,d", [(16, 12), (64, 300)])
+def test_fulldata_exchange_single_rank(C, d):
+    """The full-data path -- context on torch's stream, [grad | lp] block in a torch tensor,
+    RCCL all-reduce after every step -- on a one-rank NCCL group reproduces the plain sampler
+    bit for bit (the sum over one rank is the identity)."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from stark_amd import engine, fulldata
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        fctx = fulldata.context_on_torch_stream(0)
+        cfg = dict(num_warmup=40, num_samples=30, chains=C, seed=9)
+        m = engine.Model.synthetic(fctx, "logistic", 1, 3000, d, data_seed=4)
+        fs = fulldata.FullDataSampler(m, force_exchange=True, **cfg)
+        fs.run()
+        got = fs.draws(0)[0]
+        fs.close()
+        ref = m.sample(shard_ids=[0], **cfg)
+        np.testing.assert_array_equal(got, ref.draws[0])
+        with pytest.raises(ValueError):
+            fulldata.FullDataSampler(engine.Model.synthetic(fctx, "linear", 1, 100, 3), **cfg)
+        m.close()
+        fctx.close()
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Full-data HMC/NUTS throughput, BASELINE.json configs[4]: Bayesian logistic regression, d = 1000,
+64 chains, fp64, rows split over the GPUs of one node with a per-leapfrog gradient all-reduce
+(stark_amd/fulldata.py).
+
+N = 1e9 x d = 1000 fp64 is 8 TB of X and does not fit a node's 8 x 288 GB of HBM, so this run
+keeps --rows-per-gpu rows resident per GPU (default 2.5e7 = 200 GB; weak scaling: N = rows x
+GPUs) -- DESIGN.md section 5.  A step = one leapfrog of all 64 chains = one full-data gradient
+per chain: the two fp64-MFMA GEMM passes over the local rows (k_gemm_fwd / k_gemm_bwd), the
+chunk reduction, the all-reduce of the [64 x (Dp+1)] block over RCCL, and one NUTS
+state-machine step.  Timed: K steps after W untimed ones, from the start of sampling (a step
+costs the same whatever the sampler phase, and a config-4 chain needs far more than a bench
+window of full-data gradients to adapt, so ESS/s is not reported for this config).
+
+Usage: python tools/bench_fulldata.py [--rows-per-gpu R --steps K --warmup W];
+       N GPUs: python -m torch.distributed.run --nproc-per-node N tools/bench_fulldata.py ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFS = 78.6
+HBM_PEAK_GBS = 8000.0
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rows-per-gpu", type=float, default=2.5e7)
+    p.add_argument("--d", type=int, default=1000)
+    p.add_argument("--chains", type=int, default=64)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--seed", type=int, default=20240)
+    a = p.parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from stark_amd import engine, fulldata
+
+    rows = int(a.rows_per_gpu)
+    ctx = fulldata.context_on_torch_stream(local_rank)
+    t = time.perf_counter()
+    model = engine.Model.synthetic(ctx, "logistic", 1, rows, a.d, data_seed=a.seed, row_offset=rank * rows)
+    ctx.sync()
+    t_gen = time.perf_counter() - t
+    K, W = a.steps, a.warmup
+    fs = fulldata.FullDataSampler(model, num_warmup=1000, num_samples=100, chains=a.chains, seed=a.seed + 1)
+    if rank == 0:
+        print(f"[bench_fulldata] {world} GPU(s) x {rows} rows x d={a.d}: {model.device_bytes() / 1e9:.1f} GB/GPU, "
+              f"generated in {t_gen:.1f}s", file=sys.stderr, flush=True)
+    fs.run(1100, max_steps=W)
+
+    def barrier():
+        torch.cuda.synchronize(local_rank)
+        if world > 1:
+            dist.barrier()
+
+    ctx.set_profiling(True)
+    i0 = fs.info()
+    barrier()
+    t0 = time.perf_counter()
+    fs.run(1100, max_steps=K)
+    ctx.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    i1 = fs.info()
+    if world > 1:
+        v = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        elapsed = float(v.item())
+    steps = i1["steps"] - i0["steps"]
+    grads = i1["grad_evals"] - i0["grad_evals"]      # chain-gradients of the full data set (same on every rank)
+    sweeps = i1["sweeps"] - i0["sweeps"]
+    avg_ms = (i1["sweep_ms"] - i0["sweep_ms"]) / max(sweeps, 1)   # qT image + pass F + pass B, this rank
+    flops = 4.0 * a.d * a.chains * rows                # two GEMMs over this rank's rows
+    tfs = flops / (avg_ms * 1e-3) / 1e12
+    hbm_bytes = rows * (2 * 8 * a.d + 4 + 2 * 8 * a.chains)   # X twice, y, R written + read once
+    gbs = hbm_bytes / (avg_ms * 1e-3) / 1e9
+    line = {
+        "metric": "gradient evals/sec (whole node), full-data logistic regression d=1000, 64 chains",
+        "value": grads / elapsed, "unit": "gradient evals/sec", "n_gpus": world, "steps": K, "warmup": W,
+        "ms_per_step": 1e3 * elapsed / max(steps, 1), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (Philox in HBM, SURVEY 8d)",
+        "config": {"workload": "full-data HMC/NUTS logistic regression, per-leapfrog gradient all-reduce",
+                   "rows_total": rows * world, "rows_per_gpu": rows, "d": a.d, "chains": a.chains,
+                   "parallelism": f"row-dp{world}", "note": "N=1e9 (8 TB) exceeds node HBM; rows per GPU resident"},
+        "rows_x_chains_per_sec": grads * rows * world / elapsed,
+        "ess_per_sec": None,
+        "roofline": {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": tfs / FP64_PEAK_TFS, "traffic": None,
+                     "kernel": "k_gemm_fwd + k_gemm_bwd (fp64 MFMA 16x16x4, 64 chains)", "avg_launch_ms": avg_ms,
+                     "algorithmic_flops_per_launch": flops,
+                     "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                             "algorithmic_bytes_per_launch": hbm_bytes}},
+        "setup_s": {"datagen": t_gen},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    fs.close()
+    model.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
