@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=4000)
     p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--family", choices=["logistic", "linear"], default="logistic",
+                   help="linear --rows 1e7 --d 50: BASELINE configs[2]")
     p.add_argument("--rows", type=float, default=1e8, help="total rows N over all shards")
     p.add_argument("--d", type=int, default=100)
     p.add_argument("--shards", type=int, default=8)
@@ -61,7 +63,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(d, rows_per_shard, shards, seconds):
+def cpu_baseline(d, rows_per_shard, shards, seconds, family="logistic"):
     """The oracle's logistic gradient (oracle/stark_oracle.c, gcc -O2, scalar) run as the
     reference's execution model: one single-chain worker per shard, min(shards, cores)
     concurrent (Spark local[*]).  Each worker times full gradient evaluations over a bounded
@@ -71,25 +73,32 @@ def cpu_baseline(d, rows_per_shard, shards, seconds):
     workers = max(1, min(shards, cores))
     ctx = mp.get_context("spawn")
     with ctx.Pool(workers) as pool:
-        rates = pool.starmap(_cpu_worker, [(d, seconds, w) for w in range(workers)])
+        rates = pool.starmap(_cpu_worker, [(d, seconds, w, family) for w in range(workers)])
     sample_rows = rates[0][1]
     per_worker_grads = [r[0] * sample_rows / rows_per_shard for r in rates]   # full-shard grads/s
     return {"value": float(sum(per_worker_grads)), "unit": "gradient evals/sec (whole node)",
             "cores": workers, "kind": "port",
-            "sample": f"oracle orc_logreg_lpgrad (C, 1 thread/worker) on {sample_rows} rows x d={d} per worker, "
+            "sample": f"oracle {'orc_logreg_lpgrad' if family == 'logistic' else 'orc_linreg_lpgrad'} "
+                      f"(C, 1 thread/worker) on {sample_rows} rows x d={d} per worker, "
                       f"{seconds:.0f}s per worker, {workers} concurrent workers (one per shard, Spark local[*] model), "
                       f"scaled linearly to {rows_per_shard:.3g} rows/shard; analytic gradient (optimistic vs Stan autodiff)"}
 
 
-def _cpu_worker(d, seconds, w):
+def _cpu_worker(d, seconds, w, family="logistic"):
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     rows = 100_000
     X = O.gen_x(99, w * rows, rows, d)
     beta = O.gen_beta(99, d)
-    y, _ = O.gen_y_logistic(99, w * rows, X, 0.0, beta)
-    m = O.Model(O.FAM_LOGREG, X=X, y=y)
-    q = np.concatenate([[0.0], beta * 0.9])
+    if family == "logistic":
+        y, _ = O.gen_y_logistic(99, w * rows, X, 0.0, beta)
+        m = O.Model(O.FAM_LOGREG, X=X, y=y)
+        q = np.concatenate([[0.0], beta * 0.9])
+    else:
+        y = O.gen_y_linear(99, w * rows, X, 0.0, beta)
+        y = y[0] if isinstance(y, tuple) else y
+        m = O.Model(O.FAM_LINREG, X=X, y=y)
+        q = np.concatenate([[0.0], beta * 0.9, [0.0]])
     m.lpgrad(q)
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -119,7 +128,7 @@ def main():
     ctx = engine.Context(local_rank)
 
     t = time.perf_counter()
-    model = engine.Model.synthetic(ctx, "logistic", spr, rows_per_shard, a.d, data_seed=a.seed,
+    model = engine.Model.synthetic(ctx, a.family, spr, rows_per_shard, a.d, data_seed=a.seed,
                                    row_offset=first * rows_per_shard)
     ctx.sync()
     t_gen = time.perf_counter() - t
@@ -254,7 +263,9 @@ def main():
     # C <= 4: k_sweep3 (VALU), bound by HBM.
     mfma = a.chains == 16
     kname = "k_sweepm" if mfma else "k_sweep3"
-    bytes_per_shard = rows_per_shard * (8 * a.d + 4)        # X fp64 + y int32, once per sweep
+    ybytes = 4 if a.family == "logistic" else 8
+    fam = "LOGREG" if a.family == "logistic" else "LINREG"
+    bytes_per_shard = rows_per_shard * (8 * a.d + ybytes)   # X fp64 + y (int32 / fp64), once per sweep
     avg_ms = sweep_ms / max(sweeps, 1)
     shards_per_launch = shard_sweeps / max(sweeps, 1)
     bytes_per_launch = bytes_per_shard * shards_per_launch
@@ -276,20 +287,20 @@ def main():
     if mfma:
         roof = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": (tfs / FP64_PEAK_TFS) if tfs else None, "traffic": traffic,
-                "kernel": f"k_sweepm<LOGREG> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
+                "kernel": f"k_sweepm<{fam}> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
                 "algorithmic_flops_per_launch": flops_per_launch, "algorithmic_bytes_per_launch": bytes_per_launch,
                 "hbm": hbm, "fp64_measured_ceiling_tfs": FP64_MEASURED_TFS}
     else:
         roof = dict(bound="hbm", **{k: v for k, v in hbm.items()}, traffic=traffic,
-                    kernel=f"k_sweep3<LOGREG,{a.chains}>", avg_launch_ms=avg_ms,
+                    kernel=f"k_sweep3<{fam},{a.chains}>", avg_launch_ms=avg_ms,
                     algorithmic_bytes_per_launch=bytes_per_launch)
     cpu = None
     if not a.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(a.d, rows_per_shard, a.shards, a.cpu_baseline_seconds)
+        cpu = cpu_baseline(a.d, rows_per_shard, a.shards, a.cpu_baseline_seconds, a.family)
 
     value = grads / elapsed
     line = {
-        "metric": "gradient evals/sec (whole node), logistic regression N=1e8 d=100",
+        "metric": f"gradient evals/sec (whole node), {a.family} regression N={a.rows:.0e} d={a.d}".replace("e+0", "e"),
         "value": value,
         "unit": "gradient evals/sec",
         "n_gpus": world,
@@ -301,7 +312,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (Philox in HBM, SURVEY 8d)",
-        "config": {"workload": "bayesian logistic regression, 8 subposterior shards + consensus combine",
+        "config": {"workload": f"bayesian {a.family} regression, {a.shards} subposterior shards + consensus combine",
                    "rows": int(a.rows), "d": a.d, "shards": a.shards, "shards_per_gpu": spr,
                    "chains_per_shard": a.chains, "adapt_iters": A, "stepsize_jitter": a.stepsize_jitter,
                    "parallelism": f"shard-dp{world}"},

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""8-schools with 4096 parallel NUTS chains on one MI355X (BASELINE.json configs[1]).
+
+The data are example/stark_ex.py:4-6 (J = 8, embedded here: /root/reference does not exist on
+the GPU box); the program is example/schools.stan (non-centred: mu, tau, eta[J]).  All 4096
+chains run Stan's defaults (1000 warmup with adaptation + 1000 draws) in the fused kernel
+(k_nuts_fused_schools: one wave per chain, the O(J) gradient inline, up to 4096 leapfrogs per
+launch).  Reported: chain-gradient evaluations per second over the whole run and over the
+sampling phase, and ESS/s of the sampling phase (min over mu, tau, eta, theta of Stan 2.19's
+multi-chain ESS over all 4096 chains).
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+Y = [28.0, 8.0, -3.0, 7.0, -1.0, 1.0, 18.0, 12.0]        # example/stark_ex.py:5
+SIGMA = [15.0, 10.0, 16.0, 11.0, 9.0, 11.0, 10.0, 18.0]  # example/stark_ex.py:6
+
+
+def main():
+    import argparse
+    p = argparse.ArgumentParser()
+    p.add_argument("--chains", type=int, default=4096)
+    p.add_argument("--warmup", type=int, default=1000)
+    p.add_argument("--samples", type=int, default=1000)
+    p.add_argument("--seed", type=int, default=7)
+    a = p.parse_args()
+    from stark_amd import diagnostics, engine
+    ctx = engine.Context(0)
+    m = engine.Model(ctx, "schools", [{"y": np.array(Y), "sigma": np.array(SIGMA)}])
+    s = m.sampler(num_warmup=a.warmup, num_samples=a.samples, chains=a.chains, seed=a.seed)
+    ctx.sync()
+    t0 = time.perf_counter()
+    s.run(a.warmup)
+    ctx.sync()
+    t1 = time.perf_counter()
+    i1 = s.info()
+    s.run()
+    ctx.sync()
+    t2 = time.perf_counter()
+    i2 = s.info()
+    draws, stats = s.draws(0)
+    P = draws.shape[0]
+    e = diagnostics.ess_matrix(draws[:-1], a.chains)      # drop lp__
+    min_ess = float(np.nanmin(e))
+    samp = t2 - t1
+    line = {
+        "metric": "gradient evals/sec, 8-schools 4096 NUTS chains (1 GPU)",
+        "value": (i2["grad_evals"] - i1["grad_evals"]) / samp, "unit": "gradient evals/sec",
+        "n_gpus": 1, "higher_is_better": True, "dtype": "f64", "data": "example/stark_ex.py 8-schools",
+        "config": {"workload": "8-schools non-centred, NUTS diag_e, Stan defaults", "chains": a.chains,
+                   "num_warmup": a.warmup, "num_samples": a.samples, "P": P},
+        "grad_evals_per_sec_whole_run": i2["grad_evals"] / (t2 - t0),
+        "ess_per_sec_sampling": min_ess / samp, "min_ess": min_ess,
+        "seconds": {"warmup": t1 - t0, "sampling": samp},
+        "leapfrogs_per_transition": (i2["leapfrogs"] - i1["leapfrogs"]) / (a.chains * a.samples),
+        "divergent": i2["divergent"], "accept_stat_mean": float(stats[:, 0].mean()),
+        "posterior_mean_mu_tau": [float(draws[0].mean()), float(draws[1].mean())],
+    }
+    print(json.dumps(line), flush=True)
+    s.close()
+    m.close()
+
+
+if __name__ == "__main__":
+    main()
