@@ -781,7 +781,7 @@ __device__ __forceinline__ void softplus_tab(double ntt, const double* tab, doub
 
 // ABL (micro-benchmark ablations only): bit 0 linear residual stand-in, bit 1 no backward,
 // bit 2 no forward.  KFS/JTS: compile-time KF / JT for the BASELINE shapes (0 = runtime).
-template <int FAM, int KFS = 0, int JTS = 0, int ABL = 0, int MINB = SM_MINB>
+template <int FAM, int KFS = 0, int JTS = 0, int ABL = 0, int MINB = SM_MINB, bool VREM = false>
 __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
   constexpr int C = SM_C, NW = SM_W;
   constexpr int KFM = KFS ? KFS : 32, JTM = JTS ? JTS : 8;
@@ -848,6 +848,11 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
 #pragma unroll
   for (int t = 0; t < JTM; ++t) gacc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
   double lpa = 0.0, gaa = 0.0;
+  // VREM: the last column tile holds d - 16 (JT - 1) <= 4 columns (d = 100: 96..99, d = 50: 48, 49);
+  // 4 MFMAs for it would be >= 75 % padding, so the VALU does them (16 FMAs per lane): gv[jj] =
+  // column 16 (JT - 1) + jj, chain lr, summed over this lane's 4 rows (rows lh + 4i)
+  constexpr int JTMM = VREM ? JTM - 1 : JTM;
+  double gv[4] = {0.0, 0.0, 0.0, 0.0};
 
   // Ring of NB slots per wave: sub-tiles k+1 .. k+NB-1 are in flight while sub-tile k is
   // computed (NB = 1: the DMA of sub-tile k is issued when sub-tile k-1 is done, and the
@@ -917,8 +922,21 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
 #pragma unroll
-        for (int t = 0; t < JTM; ++t) {
+        for (int t = 0; t < JTMM; ++t) {
           if (t < JT) gacc[t] = mfma_f64(xs[(lh + 4 * s) * d + std::min(16 * t + lr, d - 1)], de[s], gacc[t]);
+        }
+      }
+      if constexpr (VREM) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          // 16-B aligned: d and 16 (JT - 1) are even; columns past d read the next row / the y
+          // area and are never written out
+          const dbl2* xv = reinterpret_cast<const dbl2*>(xs + (lh + 4 * i) * d + 16 * (JTM - 1));
+          const dbl2 a0 = xv[0], a1 = xv[1];
+          gv[0] = fma(a0.x, de[i], gv[0]);
+          gv[1] = fma(a0.y, de[i], gv[1]);
+          gv[2] = fma(a1.x, de[i], gv[2]);
+          gv[3] = fma(a1.y, de[i], gv[3]);
         }
       }
     }
@@ -930,7 +948,7 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
   double* red = lds;                                   // [NW][JT*16 columns][16 chains]
   const int JC = JT * 16;
 #pragma unroll
-  for (int t = 0; t < JTM; ++t) {
+  for (int t = 0; t < JTMM; ++t) {
     if (t < JT) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) red[((size_t)w * JC + 16 * t + lh + 4 * i) * 16 + lr] = gacc[t][i];
@@ -939,12 +957,23 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
   double* red2 = red + (size_t)NW * JC * 16;           // [NW][64 lanes][lp, g_alpha]
   red2[(size_t)tid * 2 + 0] = lpa;
   red2[(size_t)tid * 2 + 1] = gaa;
+  double* red3 = red2 + (size_t)NW * 64 * 2;           // VREM: [NW][4 lh][4 jj][16 chains]
+  if constexpr (VREM) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) red3[((size_t)(w * 4 + lh) * 4 + jj) * 16 + lr] = gv[jj];
+  }
   __syncthreads();
   double* out = A.partial + ((size_t)shard * A.Gs + chunk) * C * A.PW;
+  const int jv = VREM ? 16 * (JT - 1) : d;             // first column summed from red3
   for (int i = tid; i < C * d; i += NW * 64) {
     const int c = i / d, j = i % d;
     double v = 0.0;
-    for (int ww = 0; ww < NW; ++ww) v += red[((size_t)ww * JC + j) * 16 + c];
+    if (j < jv) {
+      for (int ww = 0; ww < NW; ++ww) v += red[((size_t)ww * JC + j) * 16 + c];
+    } else {
+      for (int ww = 0; ww < NW; ++ww)
+        for (int h = 0; h < 4; ++h) v += red3[((size_t)(ww * 4 + h) * 4 + (j - jv)) * 16 + c];
+    }
     out[(size_t)c * A.PW + 1 + j] = v;
   }
   if (tid < 2 * C) {          // chain c: lanes h*16 + c of every wave, in (wave, h) order
@@ -1146,8 +1175,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm_fwd(SweepArgs A) {
 // Pass B: one block per (shard, chunk, 64-column block); G[j][c] += X[r][j] R[r][c] over the
 // chunk's rows, straight into the chunk's partial row (columns 1 .. d).
 __global__ __launch_bounds__(256, 2) void k_gemm_bwd(SweepArgs A, int njb) {
-  const int jb = blockIdx.x % njb;
-  const int sc = blockIdx.x / njb;
+  // XCD-aware order: blocks are dealt to the 8 XCDs round-robin (blockIdx % 8), so the njb
+  // column blocks of a chunk get blockIdx values of one residue -- one XCD, whose L2 then
+  // serves the chunk's R rows to all of them (else each XCD re-reads R from HBM)
+  const int NS = gridDim.x / njb;
+  int sc, jb;
+  if ((NS & 7) == 0) {
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    sc = x + 8 * (k / njb);
+    jb = k % njb;
+  } else {
+    jb = blockIdx.x % njb;
+    sc = blockIdx.x / njb;
+  }
   const int shard = A.shard0 + sc / A.G;
   const int chunk = sc % A.G;
   if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
@@ -1331,7 +1371,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *G = (int)g;
     const int JT = (d + 15) / 16;
     const size_t ring = (size_t)SM_W * nb * sweepm_slot_bytes(d) + SP_TAB * sizeof(double);
-    const size_t red = ((size_t)SM_W * JT * 16 * 16 + (size_t)SM_W * 64 * 2) * sizeof(double);
+    const size_t red = ((size_t)SM_W * JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * sizeof(double);
     *lds_bytes = std::max(ring, red);
     return;
   }
@@ -1443,8 +1483,8 @@ static hipError_t launch_sweepm(const SweepArgs& A, int d, int nblocks, size_t l
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A, A.LD);
     return hipGetLastError();
   };
-  if (d == 100) return go(k_sweepm<FAM, 25, 7>);
-  if (d == 50) return go(k_sweepm<FAM, 13, 4>);
+  if (d == 100) return go(k_sweepm<FAM, 25, 7, 0, SM_MINB, true>);
+  if (d == 50) return go(k_sweepm<FAM, 13, 4, 0, SM_MINB, true>);
   return go(k_sweepm<FAM>);
 }
 

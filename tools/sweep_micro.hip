@@ -274,10 +274,10 @@ int main(int argc, char** argv) {
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       timeit("v4 1blk nb3", bytes, [&] { hipLaunchKernelGGL(kern, dim3(nsh * G), dim3(256), l1, st, A1, nb1); });
     }
-    abl("v4 -trans", k_sweepm<STK_LOGREG, 25, 7, 1>);
-    abl("v4 -bwd", k_sweepm<STK_LOGREG, 25, 7, 2>);
-    abl("v4 -fwd", k_sweepm<STK_LOGREG, 25, 7, 4>);
-    abl("v4 -all", k_sweepm<STK_LOGREG, 25, 7, 7>);
+    abl("v4 -trans", k_sweepm<STK_LOGREG, 25, 7, 1, SM_MINB, true>);
+    abl("v4 -bwd", k_sweepm<STK_LOGREG, 25, 7, 2, SM_MINB, true>);
+    abl("v4 -fwd", k_sweepm<STK_LOGREG, 25, 7, 4, SM_MINB, true>);
+    abl("v4 -all", k_sweepm<STK_LOGREG, 25, 7, 7, SM_MINB, true>);
     const double fl = 4.0 * d * C * (double)rows * nsh;   // algorithmic fp64 flops of one sweep
     timeit("v4 flops", fl, [&] {
       CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st, wsp));
