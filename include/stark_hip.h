@@ -137,6 +137,10 @@ STK_API int stk_model_create_synthetic(stk_ctx* ctx, int family, int nshards, in
                                        double alpha, const double* beta, double noise_sigma,
                                        stk_model** out);
 STK_API int stk_gen_beta(uint64_t data_seed, int32_t n_cols, double* beta);   /* host, beta ~ N(0, 1/d) */
+/* Regressions: alpha ~ normal(0, alpha_scale), beta ~ normal(0, beta_scale) (each 0 or inf = flat,
+ * the default) -- the priors of a `model` block the front end recognises (stark/stark.py:37-39
+ * setStanModel of such a program).  Applies to every shard, before sampling. */
+STK_API int stk_model_set_prior(stk_model* m, double alpha_scale, double beta_scale);
 STK_API int stk_model_destroy(stk_model* m);
 STK_API int stk_model_info(const stk_model* m, int shard, int32_t* D, int32_t* P, int64_t* n_rows);
 STK_API int stk_model_copy_data(stk_model* m, int shard, double* x, double* y, int32_t* y_int);
@@ -172,7 +176,7 @@ STK_API int stk_sampler_destroy(stk_sampler* s);
  * identical inputs, so chain states stay identical without any other exchange.  dev_block:
  * NULL (the library's block), or caller-allocated device memory of `count` doubles used in
  * its place -- e.g. a torch tensor that torch.distributed.all_reduce sums over RCCL.  Logistic
- * family only (its log density is a pure sum over rows); call before the first run.
+ * family with flat priors only (its log density is a pure sum over rows); call before the first run.
  * No reference counterpart (SURVEY.md 8e "full-data extension"). */
 typedef int (*stk_allreduce_fn)(void* user, double* block, int64_t count, void* stream);
 STK_API int stk_sampler_grad_block(stk_sampler* s, int64_t* count);

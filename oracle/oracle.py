@@ -64,6 +64,8 @@ def lib():
         L.orc_logreg_lpgrad.restype = ctypes.c_double
         L.orc_linreg_lpgrad.argtypes = [i64, ci, dp, dp, dp, dp]
         L.orc_linreg_lpgrad.restype = ctypes.c_double
+        L.orc_prior_lpgrad.argtypes = [ctypes.c_double, ctypes.c_double, ci, dp, dp]
+        L.orc_prior_lpgrad.restype = ctypes.c_double
         L.orc_run_chain.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u32, dp, dp, dp, dp, dp]
         L.orc_run_chain.restype = ctypes.c_long
         L.orc_transition.argtypes = [ctypes.c_void_p, u64, u32, u32, ci, ctypes.c_double, dp, dp, dp, dp]
@@ -125,7 +127,7 @@ def gen_y_linear(seed, row0, X, alpha, beta, sigma=1.0):
 class _Data(ctypes.Structure):
     _fields_ = [("family", ctypes.c_int), ("n", ctypes.c_int64), ("d", ctypes.c_int),
                 ("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("yi", ctypes.c_void_p),
-                ("sigma", ctypes.c_void_p)]
+                ("sigma", ctypes.c_void_p), ("pa", ctypes.c_double), ("pb", ctypes.c_double)]
 
 
 class _Cfg(ctypes.Structure):
@@ -139,7 +141,8 @@ class _Cfg(ctypes.Structure):
 class Model:
     """Holds host arrays for one shard and exposes lp/grad and the NUTS twin."""
 
-    def __init__(self, family, *, y=None, sigma=None, X=None):
+    def __init__(self, family, *, y=None, sigma=None, X=None, prior_alpha=0.0, prior_beta=0.0):
+        """prior_alpha / prior_beta: scales s of normal(0, s) priors on alpha / beta (0: flat)."""
         self.family = family
         if family == FAM_SCHOOLS:
             self.y = np.ascontiguousarray(y, np.float64)
@@ -161,7 +164,8 @@ class Model:
                         self.X.ctypes.data if self.X is not None else None,
                         self.y.ctypes.data if family != FAM_LOGREG else None,
                         self.y.ctypes.data if family == FAM_LOGREG else None,
-                        self.sigma.ctypes.data if self.sigma is not None else None)
+                        self.sigma.ctypes.data if self.sigma is not None else None,
+                        1.0 / prior_alpha ** 2 if prior_alpha else 0.0, 1.0 / prior_beta ** 2 if prior_beta else 0.0)
 
     def lpgrad(self, q):
         q = np.ascontiguousarray(q, np.float64)
@@ -173,6 +177,8 @@ class Model:
             lp = L.orc_logreg_lpgrad(self.n, self.d, _dp(self.X), _ip(self.y), _dp(q), _dp(g))
         else:
             lp = L.orc_linreg_lpgrad(self.n, self.d, _dp(self.X), _dp(self.y), _dp(q), _dp(g))
+        if self.family != FAM_SCHOOLS and (self._s.pa or self._s.pb):
+            lp += L.orc_prior_lpgrad(self._s.pa, self._s.pb, self.d, _dp(q), _dp(g))
         return lp, g
 
     def run_chain(self, *, num_warmup=1000, num_samples=1000, max_depth=10, adapt_delta=0.8,

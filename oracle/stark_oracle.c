@@ -171,6 +171,7 @@ typedef struct {
   const double* y;  /* schools / linreg */
   const int32_t* yi;/* logreg */
   const double* sigma; /* schools */
+  double pa, pb;    /* regressions: precisions 1/s^2 of alpha ~ normal(0, s_a), beta ~ normal(0, s_b); 0 = flat */
 } orc_data;
 
 int orc_dim(const orc_data* m) {
@@ -250,13 +251,28 @@ double orc_linreg_lpgrad(int64_t N, int d, const double* X, const double* y, con
   return -0.5 * ss - (double)N * u + u;
 }
 
+/* Stan `alpha ~ normal(0, s_a); beta ~ normal(0, s_b);` with propto=true (constants dropped):
+ * lp -= (pa alpha^2 + pb |beta|^2) / 2, grad -= p q.  q = (alpha, beta[1..d], ...). */
+double orc_prior_lpgrad(double pa, double pb, int d, const double* q, double* grad) {
+  double sb = 0.0;
+  for (int j = 1; j <= d; ++j) sb += q[j] * q[j];
+  if (grad) {
+    grad[0] -= pa * q[0];
+    for (int j = 1; j <= d; ++j) grad[j] -= pb * q[j];
+  }
+  return -0.5 * (pa * q[0] * q[0] + pb * sb);
+}
+
 double orc_lpgrad(const orc_data* m, const double* q, double* grad) {
+  double lp;
   switch (m->family) {
     case FAM_SCHOOLS: return orc_schools_lpgrad((int)m->n, m->y, m->sigma, q, grad);
-    case FAM_LINREG: return orc_linreg_lpgrad(m->n, m->d, m->x, m->y, q, grad);
-    case FAM_LOGREG: return orc_logreg_lpgrad(m->n, m->d, m->x, m->yi, q, grad);
+    case FAM_LINREG: lp = orc_linreg_lpgrad(m->n, m->d, m->x, m->y, q, grad); break;
+    case FAM_LOGREG: lp = orc_logreg_lpgrad(m->n, m->d, m->x, m->yi, q, grad); break;
+    default: return NAN;
   }
-  return NAN;
+  if (m->pa != 0.0 || m->pb != 0.0) lp += orc_prior_lpgrad(m->pa, m->pb, m->d, q, grad);
+  return lp;
 }
 
 /* ------------------------------------------------------- NUTS (Stan 2.19.1) */

@@ -77,6 +77,7 @@ SIGNATURES = [
     ("stk_model_create_synthetic", ctypes.c_int,
      [_vp, ctypes.c_int, ctypes.c_int, _i64, _i64, _i32, _u64, _dbl, _vp, _dbl, _pp]),
     ("stk_gen_beta", ctypes.c_int, [_u64, _i32, _vp]),
+    ("stk_model_set_prior", ctypes.c_int, [_vp, _dbl, _dbl]),
     ("stk_model_destroy", ctypes.c_int, [_vp]),
     ("stk_model_info", ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
                                       ctypes.POINTER(_i64)]),

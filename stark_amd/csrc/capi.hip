@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "common.h"
+#include <cmath>
 
 using namespace stk;
 
@@ -776,6 +777,20 @@ int stk_sampler_run(stk_sampler* s, int32_t target_iter, int64_t max_steps) {
   return STK_OK;
 }
 
+int stk_model_set_prior(stk_model* m, double alpha_scale, double beta_scale) {
+  ARG_CHECK(m, "stk_model_set_prior: NULL model");
+  ARG_CHECK(m->family == STK_LOGREG || m->family == STK_LINREG, "priors apply to the regression families");
+  ARG_CHECK(alpha_scale >= 0.0 && beta_scale >= 0.0, "prior scales must be >= 0 (0 or inf: flat)");
+  auto prec = [](double sc) { return (sc == 0.0 || std::isinf(sc)) ? 0.0 : 1.0 / (sc * sc); };
+  for (auto& sd : m->sh) {
+    sd.pa = prec(alpha_scale);
+    sd.pb = prec(beta_scale);
+  }
+  STK_HIP_CHECK(hipSetDevice(m->ctx->device));
+  STK_HIP_CHECK(hipMemcpy(m->sh_dev.p, m->sh.data(), sizeof(ShardDev) * m->sh.size(), hipMemcpyHostToDevice));
+  return STK_OK;
+}
+
 int stk_sampler_grad_block(stk_sampler* s, int64_t* count) {
   ARG_CHECK(s && count, "stk_sampler_grad_block: bad arguments");
   *count = (int64_t)s->A.nchains * (s->A.Dp + 1);
@@ -787,6 +802,8 @@ int stk_sampler_set_allreduce(stk_sampler* s, stk_allreduce_fn fn, void* user, d
   ARG_CHECK(s->m->family == STK_LOGREG,
             "full-data mode needs a purely additive log density (logistic: flat priors, no Jacobian term)");
   ARG_CHECK(s->step == 0, "stk_sampler_set_allreduce: call before the first stk_sampler_run");
+  for (const auto& sd : s->m->sh)
+    ARG_CHECK(sd.pa == 0.0 && sd.pb == 0.0, "full-data mode: flat priors only (a prior would be summed once per rank)");
   const size_t n = (size_t)s->A.nchains * (s->A.Dp + 1);
   if (dev_block) {
     STK_HIP_CHECK(hipSetDevice(s->m->ctx->device));

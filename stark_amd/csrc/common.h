@@ -37,6 +37,7 @@ struct ShardDev {
   int d;                // covariates
   int D;                // unconstrained dimension
   int P;                // output columns (params + transformed params + lp__)
+  double pa, pb;        // regressions: prior precisions 1/s^2 of alpha ~ normal(0, s_a), beta ~ normal(0, s_b) (0: flat)
 };
 
 // Workspace of the two-pass (v5, 64-chain) sweep: beta^T images and the residual matrix.

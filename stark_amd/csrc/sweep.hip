@@ -1286,17 +1286,30 @@ __global__ __launch_bounds__(256) void k_sweep_reduce(SweepArgs A, double* lp_ou
   const double t = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
   const size_t gid = (size_t)shard * C + c;
   double* g = g_out + gid * A.Dp;
+  const double* qc = A.q + gid * A.Dp;
+  // normal(0, s) priors on alpha (q[0]) and beta (q[1..d]): lp -= pa a^2/2 + pb |b|^2/2 (Stan's
+  // propto drops the constants), d/dq -= p q.  Flat (pa = pb = 0): no change, bit for bit.
+  double prior_g = 0.0, prior_lp = 0.0;
+  if (sh.pa != 0.0 || sh.pb != 0.0) {
+    if (o == 0) prior_g = -sh.pa * qc[0];
+    else if (o <= d) prior_g = -sh.pb * qc[o];
+    else {
+      double sb = 0.0;
+      for (int j = 1; j <= d; ++j) sb = fma(qc[j], qc[j], sb);
+      prior_lp = -0.5 * (sh.pa * qc[0] * qc[0] + sh.pb * sb);
+    }
+  }
   if (FAM == STK_LOGREG) {
-    if (o == d + 1) lp_out[gid] = t;
-    else g[o] = t;
+    if (o == d + 1) lp_out[gid] = t + prior_lp;
+    else g[o] = t + prior_g;
   } else {
-    const double u = A.q[gid * A.Dp + d + 1];
+    const double u = qc[d + 1];
     const double N = (double)sh.n;
     if (o == d + 1) {
       g[d + 1] = -N + t + 1.0;
-      lp_out[gid] = -0.5 * t - N * u + u;
+      lp_out[gid] = -0.5 * t - N * u + u + prior_lp;
     } else {
-      g[o] = t;
+      g[o] = t + prior_g;
     }
   }
 }

@@ -257,6 +257,12 @@ class Model:
         check(_lib.load().stk_log_density_grad(self._h, shard, q.ctypes.data, C, lp.ctypes.data, g.ctypes.data))
         return lp, g
 
+    def set_prior(self, alpha=None, beta=None):
+        """normal(0, s) priors on alpha and beta (regressions); None or 0: flat."""
+        check(_lib.load().stk_model_set_prior(self._h, float(alpha or 0.0), float(beta or 0.0)))
+        self.prior = {"alpha": alpha, "beta": beta}
+        return self
+
     def sampler(self, **cfg) -> "Sampler":
         return Sampler(self, make_config(**cfg))
 

@@ -49,14 +49,48 @@ def _stmts(block: str) -> list:
     return [s for s in block.split(";") if s]
 
 
-def recognise(model_code: str) -> str:
-    """Return 'schools', 'linear' or 'logistic' for a supported Stan program."""
+_NUM = r"([0-9]+(?:\.[0-9]*)?(?:[eE][-+]?[0-9]+)?|\.[0-9]+(?:[eE][-+]?[0-9]+)?)"
+_PRIOR = re.compile(r"(alpha|beta)~normal\(0(?:\.0*)?," + _NUM + r"\)$")
+
+
+def _split_priors(stmts):
+    """Separate `alpha ~ normal(0, s)` / `beta ~ normal(0, s)` statements (s > 0) from the rest."""
+    priors, rest = {}, []
+    for st in stmts:
+        m = _PRIOR.match(st)
+        if m and float(m.group(2)) > 0 and m.group(1) not in priors:
+            priors[m.group(1)] = float(m.group(2))
+        else:
+            rest.append(st)
+    return priors, rest
+
+
+def program_info(model_code: str):
+    """(family, priors) of a supported Stan program; priors = {'alpha': s, 'beta': s} for the
+    regressions' optional `alpha ~ normal(0, s)` / `beta ~ normal(0, s)` statements (absent: flat)."""
     code = _strip(model_code)
     b = _blocks(code)
+    priors, rest = _split_priors(_stmts(b.get("model", "")))
+    fam = _recognise_blocks(b, sorted(rest))
+    if fam == "schools" and priors:
+        fam = None
+    if fam is None:
+        raise NotImplementedError(
+            "stark_amd runs a fixed set of model families on the GPU (8 schools, Bayesian linear and logistic "
+            "regression with flat or normal(0, s) priors on alpha and beta; see stark_amd/models/*.stan).  This "
+            "Stan program is not one of them; pass family='schools'|'linear'|'logistic' if it is an equivalent "
+            "program.")
+    return fam, priors
+
+
+def recognise(model_code: str) -> str:
+    """Return 'schools', 'linear' or 'logistic' for a supported Stan program."""
+    return program_info(model_code)[0]
+
+
+def _recognise_blocks(b: dict, stm: list):
     params = b.get("parameters", "")
-    model = b.get("model", "")
     tp = b.get("transformed parameters", "")
-    stm = sorted(_stmts(model))
     # 8 schools, non-centred (example/schools.stan:1-18)
     if (_decl(params, r"(^|;)real mu(;|$)") and _decl(params, r"real<lower=0>tau") and
             _decl(params, r"(real eta\[J\]|vector\[J\]eta|array\[J\]real eta)")):
@@ -72,24 +106,27 @@ def recognise(model_code: str) -> str:
         if stm in (["y~normal(alpha+x*beta,sigma)"], ["y~normal(x*beta+alpha,sigma)"]):
             if _decl(params, r"real<lower=0>sigma"):
                 return "linear"
-    raise NotImplementedError(
-        "stark_amd runs a fixed set of model families on the GPU (8 schools, Bayesian linear and logistic "
-        "regression with flat priors; see stark_amd/models/*.stan).  This Stan program is not one of them; "
-        "pass family='schools'|'linear'|'logistic' if it is an equivalent program.")
+    return None
 
 
-def load_program(file=None, model_code=None, family=None, **_ignored):
-    """Mirror of pystan.StanModel(file=..., model_code=...) argument handling."""
+def load_program_info(file=None, model_code=None, family=None, priors=None, **_ignored):
+    """Mirror of pystan.StanModel(file=..., model_code=...) argument handling -> (family, priors).
+    family= (and priors={'alpha': s, 'beta': s}) override recognition."""
     if family is not None:
         if family not in ("schools", "linear", "logistic"):
             raise ValueError(f"unknown family {family!r}")
-        return family
+        return family, dict(priors or {})
     if model_code is None:
         if file is None:
             raise ValueError("Either file or model_code must be given (pystan.StanModel)")
         with open(file) as f:
             model_code = f.read()
-    return recognise(model_code)
+    return program_info(model_code)
+
+
+def load_program(file=None, model_code=None, family=None, **kw):
+    """The family of the program (stark/stark.py:37-39 setStanModel)."""
+    return load_program_info(file=file, model_code=model_code, family=family, **kw)[0]
 
 
 def pack_data(family: str, data: dict) -> dict:

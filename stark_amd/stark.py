@@ -147,11 +147,12 @@ class Stark:
         self.prepare_data_callback = prepare_data_callback
         self.n_partitions = self.rdd.getNumPartitions()
         self.family = None
+        self.priors = {}
         self.last_run = None
 
     def setStanModel(self, **kwargs):
         """stark/stark.py:37-39; accepts pystan.StanModel's file= / model_code= (+ family=)."""
-        self.family = frontend.load_program(**kwargs)
+        self.family, self.priors = frontend.load_program_info(**kwargs)
         self.stan_kwargs = kwargs
 
     # ---- per-partition sampling (stark/stark.py:41-57), batched over partitions
@@ -167,6 +168,8 @@ class Stark:
         if shard_ids is not None:
             cfg["shard_ids"] = shard_ids
         model = engine.Model(engine.default_context(), self.family, shards)
+        if getattr(self, "priors", None):
+            model.set_prior(**self.priors)
         try:
             res = model.sample(**cfg)
         finally:

@@ -147,3 +147,36 @@ def test_combine_singular_raises(ctx):
     x = np.ones((3, 50))
     with pytest.raises(LinAlgError):
         engine.consensus([x, x + 1], ctx)
+
+
+# ---------------------------------------------------------------- normal(0, s) priors
+@pytest.mark.parametrize("C", [4, 16, 64])
+@pytest.mark.parametrize("family", ["logistic", "linear"])
+def test_prior_lpgrad(ctx, orc, family, C):
+    """alpha ~ normal(0, 2.5), beta ~ normal(0, 0.3) added once per chain in the chunk reduction."""
+    from stark_amd import engine
+    rng = np.random.default_rng(C)
+    n, d = 700, 20
+    X = rng.uniform(-1.7, 1.7, (n, d))
+    beta = rng.normal(0, 1 / np.sqrt(d), d)
+    if family == "logistic":
+        y = (rng.uniform(size=n) < 1 / (1 + np.exp(-(X @ beta)))).astype(np.int32)
+        om = orc.Model(orc.FAM_LOGREG, X=X, y=y, prior_alpha=2.5, prior_beta=0.3)
+    else:
+        y = 0.3 + X @ beta + rng.normal(size=n)
+        om = orc.Model(orc.FAM_LINREG, X=X, y=y, prior_alpha=2.5, prior_beta=0.3)
+    m = engine.Model(ctx, family, [{"x": X, "y": y}]).set_prior(alpha=2.5, beta=0.3)
+    q = rng.normal(0, 0.5, (C, om.D))
+    lp, g = m.log_density_grad(0, q)
+    for c in range(C):
+        olp, og = om.lpgrad(q[c])
+        assert _rel(lp[c], olp) < RTOL_LP
+        assert np.all(np.abs(g[c] - og) <= RTOL_LP * np.maximum(np.abs(og), np.abs(og).max() * 1e-3 + 1.0))
+    m.set_prior()                      # back to flat: bit-for-bit the flat model
+    lp0, g0 = m.log_density_grad(0, q)
+    flat = engine.Model(ctx, family, [{"x": X, "y": y}])
+    lp1, g1 = flat.log_density_grad(0, q)
+    np.testing.assert_array_equal(lp0, lp1)
+    np.testing.assert_array_equal(g0, g1)
+    m.close()
+    flat.close()

@@ -70,8 +70,9 @@ def test_recognise_programs():
         frontend.recognise(newsyntax.replace("std_normal()", "normal(0, 2)"))
     prior = open(os.path.join(ROOT, "stark_amd", "models", "logistic.stan")).read().replace(
         "model {", "model {\n beta ~ normal(0, 1);")
+    assert frontend.program_info(prior) == ("logistic", {"beta": 1.0})   # normal(0, s) priors: supported
     with pytest.raises(NotImplementedError):
-        frontend.recognise(prior)
+        frontend.recognise(prior.replace("normal(0, 1)", "cauchy(0, 1)"))
 
 
 def test_pack_data_validation():
@@ -186,3 +187,18 @@ def test_ess_ar1():
     assert abs(split_rhat(x) - 1) < 0.01
     iid = rng.normal(size=(4, 5000))
     assert abs(ess(iid) / 20000 - 1) < 0.1
+
+
+def test_recognise_priors():
+    from stark_amd import frontend
+    m = os.path.join(ROOT, "stark_amd", "models")
+    assert frontend.load_program_info(file=os.path.join(m, "logistic_prior.stan")) == (
+        "logistic", {"alpha": 2.5, "beta": 1.0})
+    lin = open(os.path.join(m, "linear.stan")).read().replace("model {", "model {\n beta ~ normal(0, .5);")
+    assert frontend.program_info(lin) == ("linear", {"beta": 0.5})
+    with pytest.raises(NotImplementedError):       # non-zero prior mean: not one of the families
+        frontend.program_info(lin.replace("normal(0, .5)", "normal(1, .5)"))
+    sch = open(os.path.join(m, "schools.stan")).read().replace("model {", "model {\n alpha ~ normal(0, 1);")
+    with pytest.raises(NotImplementedError):
+        frontend.program_info(sch)
+    assert frontend.load_program_info(family="logistic", priors={"beta": 2.0}) == ("logistic", {"beta": 2.0})
