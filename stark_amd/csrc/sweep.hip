@@ -985,6 +985,199 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
   }
 }
 
+// v4e: k_sweepm for the BASELINE shapes (d = 100, 50) with an early slot release.  With one
+// 16-row slot per wave (NB = 1, two blocks per CU), k_sweepm issues the DMA of sub-tile k+1
+// only after sub-tile k is done, so each sub-tile's HBM latency is exposed and only the other
+// wave of the SIMD can cover it (PMC: MFMA busy 56 %, f64 VALU ~15 %, the rest idle).  Here
+// the backward's A operands (24 values), the remainder columns and y move to registers right
+// after the forward, the slot is refilled at once, and the residual + backward run while the
+// next sub-tile streams in.  beta moves from registers to LDS (one 16 x 4KF image per block)
+// to pay for those registers.
+#ifndef SE_NACC
+#define SE_NACC 2             // forward accumulators (4: same time, more registers; 8: spills)
+#endif
+template <int FAM, int KF, int JT, int ABL = 0>
+__global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
+  constexpr int C = SM_C, NW = SM_W, JTV = JT - 1, KP = 4 * KF;
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + 63) / 64;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * 64, r1 = std::min<int64_t>(sh.n, t1 * 64);
+  const int nrows = (int)(r1 - r0);
+  const int nsub = (nrows + SM_R - 1) / SM_R;
+  const int mine = nsub > w ? (nsub - w + NW - 1) / NW : 0;
+  constexpr int YB = (FAM == STK_LOGREG) ? 4 : 8;
+  const int SBX = SM_R * d * 8;
+  const int SS = sweepm_slot_bytes(d);
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const slot = reinterpret_cast<char*>(lds) + (size_t)w * SS;
+  double* const bimg = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);  // [16][KP]
+  double* const sptab = bimg + C * KP;
+  if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
+  const double* qs = A.q + (size_t)shard * C * A.Dp;
+  for (int i = tid; i < C * KP; i += NW * 64) {
+    const int c = i / KP, col = i % KP;
+    bimg[i] = col < d ? qs[(size_t)c * A.Dp + 1 + col] : 0.0;
+  }
+  const double alpha = qs[(size_t)lr * A.Dp];
+  const double inv_s = (FAM == STK_LINREG) ? exp(-qs[(size_t)lr * A.Dp + d + 1]) : 0.0;
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0xF70);
+
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
+  const void* ybase = (FAM == STK_LOGREG) ? (const void*)(sh.yi + r0) : (const void*)(sh.y + r0);
+  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(ybase, (int64_t)nrows * YB);
+  const int nx = (SBX + 1023) >> 10;
+  const int last_lanes = (SBX - ((nx - 1) << 10)) >> 4;
+  auto issue = [&](int k) {
+    const int u = w + NW * k;
+    const int xoff = u * SBX;
+    for (int j = 0; j < nx - 1; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(slot + j * 1024), 16, lane * 16, xoff + j * 1024, 0, 0);
+    if (lane < last_lanes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(slot + (nx - 1) * 1024), 16, lane * 16,
+                                               xoff + (nx - 1) * 1024, 0, 0);
+    if (lane < SM_R * YB / 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_vptr)(slot + SBX), 4, lane * 4, u * SM_R * YB, 0, 0);
+  };
+
+  dbl4 gacc[JTV];
+#pragma unroll
+  for (int t = 0; t < JTV; ++t) gacc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double gv[4] = {0.0, 0.0, 0.0, 0.0};
+  double lpa = 0.0, gaa = 0.0;
+  const double* xs = reinterpret_cast<const double*>(slot);
+  const double* brow = bimg + lr * KP + lh * KF;
+
+  if (mine > 0) issue(0);
+  for (int k = 0; k < mine; ++k) {
+    __builtin_amdgcn_s_waitcnt(0xF70);                   // vmcnt(0): sub-tile k landed
+    __builtin_amdgcn_sched_barrier(0);
+    const int rv = std::min(SM_R, nrows - SM_R * (w + NW * k));
+    // ---- forward
+    dbl4 ea[SE_NACC];
+#pragma unroll
+    for (int i = 0; i < SE_NACC; ++i) ea[i] = dbl4{0.0, 0.0, 0.0, 0.0};
+    if constexpr (!(ABL & 4)) {
+      const double* xrow = xs + lr * d;
+#pragma unroll
+      for (int s = 0; s < KF; ++s) ea[s % SE_NACC] = mfma_f64(xrow[std::min(lh * KF + s, d - 1)], brow[s], ea[s % SE_NACC]);
+    }
+    dbl4 e0 = ea[0], e1 = ea[1];
+#pragma unroll
+    for (int i = 2; i < SE_NACC; ++i) { if (i & 1) e1 += ea[i]; else e0 += ea[i]; }
+    // ---- everything the rest of the sub-tile needs from the slot, into registers
+    double xa[4][JTV];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < JTV; ++t) xa[s][t] = xs[(lh + 4 * s) * d + 16 * t + lr];
+    dbl2 xv[4][2];
+    double yv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const dbl2* p = reinterpret_cast<const dbl2*>(xs + (lh + 4 * i) * d + 16 * JTV);
+      xv[i][0] = p[0];
+      xv[i][1] = p[1];
+      yv[i] = (FAM == STK_LOGREG) ? (double)*reinterpret_cast<const int32_t*>(slot + SBX + (lh + 4 * i) * 4)
+                                  : *reinterpret_cast<const double*>(slot + SBX + (lh + 4 * i) * 8);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): the slot is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + 1 < mine) issue(k + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const dbl4 eta4 = e0 + e1;
+
+    // ---- residual
+    double de[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool valid = lh + 4 * i < rv;
+      const double eta = eta4[i] + alpha;
+      double dv, lt;
+      if constexpr (ABL & 1) {
+        dv = (2.0 * yv[i] - 1.0) - 0.25 * eta;
+        lt = -dv * dv;
+      } else if constexpr (FAM == STK_LOGREG) {
+        const double sgn = 2.0 * yv[i] - 1.0;
+        const double ntt = sgn * eta;
+        double e, lm, wt;
+        softplus_tab(ntt, sptab, &e, &lm, &wt);
+        const bool hi = ntt > 20.0, lo = ntt < -20.0;
+        lt = hi ? -e : (lo ? ntt : -lm);
+        dv = sgn * (hi ? e : (lo ? 1.0 : wt));
+      } else {
+        const double z = (yv[i] - eta) * inv_s;
+        lt = z * z;
+        dv = z * inv_s;
+      }
+      dv = valid ? dv : 0.0;
+      lpa += valid ? lt : 0.0;
+      gaa += dv;
+      de[i] = dv;
+    }
+    // ---- backward
+    if constexpr (!(ABL & 2)) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < JTV; ++t) gacc[t] = mfma_f64(xa[s][t], de[s], gacc[t]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        gv[0] = fma(xv[i][0].x, de[i], gv[0]);
+        gv[1] = fma(xv[i][0].y, de[i], gv[1]);
+        gv[2] = fma(xv[i][1].x, de[i], gv[2]);
+        gv[3] = fma(xv[i][1].y, de[i], gv[3]);
+      }
+    }
+  }
+
+  // ---- fixed-order block reduction (as k_sweepm with VREM)
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __syncthreads();
+  double* red = lds;
+  constexpr int JC = JT * 16;
+#pragma unroll
+  for (int t = 0; t < JTV; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[((size_t)w * JC + 16 * t + lh + 4 * i) * 16 + lr] = gacc[t][i];
+  double* red2 = red + (size_t)NW * JC * 16;
+  red2[(size_t)tid * 2 + 0] = lpa;
+  red2[(size_t)tid * 2 + 1] = gaa;
+  double* red3 = red2 + (size_t)NW * 64 * 2;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) red3[((size_t)(w * 4 + lh) * 4 + jj) * 16 + lr] = gv[jj];
+  __syncthreads();
+  double* out = A.partial + ((size_t)shard * A.Gs + chunk) * C * A.PW;
+  const int jv = 16 * JTV;
+  for (int i = tid; i < C * d; i += NW * 64) {
+    const int c = i / d, j = i % d;
+    double v = 0.0;
+    if (j < jv) {
+      for (int ww = 0; ww < NW; ++ww) v += red[((size_t)ww * JC + j) * 16 + c];
+    } else {
+      for (int ww = 0; ww < NW; ++ww)
+        for (int h = 0; h < 4; ++h) v += red3[((size_t)(ww * 4 + h) * 4 + (j - jv)) * 16 + c];
+    }
+    out[(size_t)c * A.PW + 1 + j] = v;
+  }
+  if (tid < 2 * C) {
+    const int c = tid >> 1, kind = tid & 1;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww)
+      for (int h = 0; h < 4; ++h) v += red2[(size_t)(ww * 64 + h * 16 + c) * 2 + kind];
+    out[(size_t)c * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
+}
+
 // v5 sweep: 64 chains of a shard, any d -- two fp64 MFMA GEMM passes (BASELINE configs[4]:
 // full-data logistic regression, d = 1000, 64 chains).
 //
@@ -1383,7 +1576,8 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *LD = nb;
     *G = (int)g;
     const int JT = (d + 15) / 16;
-    const size_t ring = (size_t)SM_W * nb * sweepm_slot_bytes(d) + SP_TAB * sizeof(double);
+    size_t ring = (size_t)SM_W * nb * sweepm_slot_bytes(d) + SP_TAB * sizeof(double);
+    if (d == 100) ring = (size_t)SM_W * sweepm_slot_bytes(d) + (16 * 100 + SP_TAB) * sizeof(double);   // v4e
     const size_t red = ((size_t)SM_W * JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * sizeof(double);
     *lds_bytes = std::max(ring, red);
     return;
@@ -1496,7 +1690,12 @@ static hipError_t launch_sweepm(const SweepArgs& A, int d, int nblocks, size_t l
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A, A.LD);
     return hipGetLastError();
   };
-  if (d == 100) return go(k_sweepm<FAM, 25, 7, 0, SM_MINB, true>);
+  if (d == 100) {                     // early slot release (v4e): 2-3 % over k_sweepm here
+    auto kern = k_sweepe<FAM, 25, 7>;
+    allow_big_lds((const void*)kern);
+    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A);
+    return hipGetLastError();
+  }
   if (d == 50) return go(k_sweepm<FAM, 13, 4, 0, SM_MINB, true>);
   return go(k_sweepm<FAM>);
 }

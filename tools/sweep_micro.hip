@@ -265,6 +265,16 @@ int main(int argc, char** argv) {
       timeit(name, bytes, [&] { hipLaunchKernelGGL(kern, dim3(nsh * G), dim3(256), lds, st, A4, LD); });
     };
     abl("v4 generic", k_sweepm<STK_LOGREG, 0, 0, 0>);
+    {
+      const size_t le = std::max((size_t)SM_W * sweepm_slot_bytes(d) + 16 * 100 * 8 + SP_TAB * 8, lds);
+      auto ke = [&](const char* name, auto kern) {
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        timeit(name, bytes, [&] { hipLaunchKernelGGL(kern, dim3(nsh * G), dim3(256), le, st, A4); });
+      };
+      ke("v4e", k_sweepe<STK_LOGREG, 25, 7>);
+      ke("v4e -trans", k_sweepe<STK_LOGREG, 25, 7, 1>);
+      ke("v4e -all", k_sweepe<STK_LOGREG, 25, 7, 7>);
+    }
     {   // one block per CU, 3-slot rings
       const int nb1 = sweepm_nb(d, 1);
       SweepArgs A1 = A4;
