@@ -111,13 +111,20 @@ def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # STARK_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N-rank path on one
+    # GPU (ranks share devices round-robin); the driver's runs use RCCL, one rank per GPU
+    backend = os.environ.get("STARK_DIST_BACKEND", "nccl")
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
+        local_rank %= torch.cuda.device_count()
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     from stark_amd import diagnostics, engine
 
     assert a.shards % world == 0, "shards must divide evenly over GPUs"
@@ -186,10 +193,10 @@ def main():
     done_in_window = it1 - it0                       # transitions completed per chain
     eps, _ = sampler.adaptation()
     if dist:
-        v = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        v = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local_rank))
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         elapsed = float(v.item())
-        g = torch.tensor([grads, leaps], dtype=torch.float64, device="cuda")
+        g = torch.tensor([grads, leaps], dtype=torch.float64, device=torch.device("cuda", local_rank))
         dist.all_reduce(g, op=dist.ReduceOp.SUM)
         grads, leaps = int(g[0].item()), int(g[1].item())
 

@@ -39,12 +39,19 @@ def main():
     a = p.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # STARK_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N-rank path on one
+    # GPU (ranks share devices round-robin); the driver's runs use RCCL, one rank per GPU
+    backend = os.environ.get("STARK_DIST_BACKEND", "nccl")
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     from stark_amd import engine, fulldata
 
     rows = int(a.rows_per_gpu)
@@ -76,7 +83,7 @@ def main():
     ctx.set_profiling(False)
     i1 = fs.info()
     if world > 1:
-        v = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        v = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local_rank))
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         elapsed = float(v.item())
     steps = i1["steps"] - i0["steps"]
