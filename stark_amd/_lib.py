@@ -116,6 +116,15 @@ def load():
         raise ImportError(
             f"stark_amd: {LIB_PATH} not found -- build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback for the hot path)")
+    # One HIP runtime per process: torch's wheel bundles its own libamdhip64 (soname
+    # libamdhip64.so.7, NEEDED by torch as "libamdhip64.so").  Loaded after ours, it would be
+    # a second runtime that finds no GPU; loaded first, ours binds to it by soname.  So torch
+    # (plumbing for torch.distributed / full-data mode) is imported before the library.
+    if os.environ.get("STARK_NO_TORCH_PRELOAD") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)

@@ -28,10 +28,31 @@
 
 namespace stk {
 
+// Lane exchange of a double by DPP (VALU, a few cycles; __shfl is a ds_bpermute round trip).
+template <int CTRL>
+__device__ __forceinline__ double nuts_dpp(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// Lane l's double, as a wave-uniform (scalar) value.
+__device__ __forceinline__ double lane_d(double v, int l) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// Sum over the 64 lanes with identical bits in every lane: DPP within each 16-lane row (xor 1,
+// xor 2, half-mirror, mirror -- every lane of a row ends with the same row total, addition
+// being commutative), then the four row totals as scalars, added in row order.  The per-
+// leapfrog state machine is a chain of these; the DPP form cut 8-schools time (configs[1]).
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-  return __shfl(v, 0, WAVE);   // broadcast: identical bits in every lane
+  v += nuts_dpp<0xB1>(v);
+  v += nuts_dpp<0x4E>(v);
+  v += nuts_dpp<0x141>(v);
+  v += nuts_dpp<0x140>(v);
+  return (lane_d(v, 0) + lane_d(v, 16)) + (lane_d(v, 32) + lane_d(v, 48));
 }
 
 __device__ __forceinline__ double log_sum_exp2(double a, double b) {   // stan::math::log_sum_exp
@@ -46,8 +67,8 @@ __device__ __forceinline__ double log_sum_exp2(double a, double b) {   // stan::
 // grad lp.  Mirrors oracle orc_schools_lpgrad.
 template <int NCH>
 __device__ double schools_lpgrad(const ShardDev& sh, const double (&q)[NCH], double (&glp)[NCH], int lane, int D) {
-  const double mu = __shfl(q[0], 0, WAVE);
-  const double u = __shfl(q[0], 1, WAVE);
+  const double mu = lane_d(q[0], 0);
+  const double u = lane_d(q[0], 1);
   const double tau = exp(u);
   double lp = 0.0, smu = 0.0, su = 0.0;
 #pragma unroll
@@ -83,8 +104,8 @@ __device__ void write_draw(const NutsArgs& A, const ShardDev& sh, int shard, int
   const int D = sh.D;
   const size_t S = (size_t)A.S_total;
   if (A.family == STK_SCHOOLS) {
-    const double mu = __shfl(q[0], 0, WAVE);
-    const double tau = exp(__shfl(q[0], 1, WAVE));
+    const double mu = lane_d(q[0], 0);
+    const double tau = exp(lane_d(q[0], 1));
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       const int e = k * WAVE + lane;
@@ -116,11 +137,15 @@ struct NutsChain {
   double q[NCH], p[NCH], g[NCH], im[NCH];
 
   __device__ NutsChain(const NutsArgs& a, int gid_, int lane_)
+      : NutsChain(a, gid_, lane_, a.vec + (size_t)gid_ * V_COUNT * a.Dp,
+                  a.stk + (size_t)gid_ * a.max_depth * SV_COUNT * a.Dp) {}
+  // vec_ / stk_: this chain's vector block and tree stack (global memory, or an LDS copy)
+  __device__ NutsChain(const NutsArgs& a, int gid_, int lane_, double* vec_, double* stk_)
       : A(a), gid(gid_), lane(lane_), shard(gid_ / a.C), cidx(gid_ % a.C), D(a.shards[gid_ / a.C].D),
         rid(rng_stream(a, gid_)),
         sh(a.shards[gid_ / a.C]),
-        vec(a.vec + (size_t)gid_ * V_COUNT * a.Dp),
-        stk(a.stk + (size_t)gid_ * a.max_depth * SV_COUNT * a.Dp),
+        vec(vec_),
+        stk(stk_),
         stks(a.stks + (size_t)gid_ * a.max_depth * SS_COUNT) {}
 
   __device__ __forceinline__ bool ok(int k) const { return k * WAVE + lane < D; }
@@ -611,13 +636,26 @@ __global__ __launch_bounds__(64) void k_nuts_step(NutsArgs A, int step_id, int p
   }
 }
 
+// The chain's vector block and tree stack live in LDS for the whole launch (copied in and
+// out once): the state machine's per-leapfrog bookkeeping (z+/z-, sample point, rho, p#,
+// Welford sums, the pending sub-tree stack) then costs LDS instead of L2/HBM round trips.
 template <int NCH>
 __global__ __launch_bounds__(64) void k_nuts_fused_schools(NutsArgs A, int pause_at, int max_steps) {
   const int gid = blockIdx.x, lane = threadIdx.x;
-  NutsChain<NCH> ch(A, gid, lane);
+  extern __shared__ double fl[];
+  const size_t nv = (size_t)V_COUNT * A.Dp, ns = (size_t)A.max_depth * SV_COUNT * A.Dp;
+  double* const gvec = A.vec + (size_t)gid * nv;
+  double* const gstk = A.stk + (size_t)gid * ns;
+  {
+    const int mode0 = A.iv[(size_t)gid * I_COUNT + I_MODE];
+    if (mode0 == M_DONE || mode0 == M_ERROR) return;
+  }
+  for (size_t i = lane; i < nv; i += WAVE) fl[i] = gvec[i];
+  for (size_t i = lane; i < ns; i += WAVE) fl[nv + i] = gstk[i];
+  __syncthreads();
+  NutsChain<NCH> ch(A, gid, lane, fl, fl + nv);
   ch.load();
   const int mode = ch.iv[I_MODE];
-  if (mode == M_DONE || mode == M_ERROR) return;
   bool req;
   if (mode == M_PAUSED) {
     if (ch.iv[I_ITER] >= pause_at) return;
@@ -639,6 +677,9 @@ __global__ __launch_bounds__(64) void k_nuts_fused_schools(NutsArgs A, int pause
   ch.save();
   if (req) ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);
   if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += ngrad;
+  __syncthreads();
+  for (size_t i = lane; i < nv; i += WAVE) gvec[i] = fl[i];
+  for (size_t i = lane; i < ns; i += WAVE) gstk[i] = fl[nv + i];
 }
 
 // lp / gradient of the 8-schools density at C points of one shard (parity hook).
@@ -674,7 +715,15 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
 }
 template <int NCH>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
-  hipLaunchKernelGGL(k_nuts_fused_schools<NCH>, dim3(A.nchains), dim3(64), 0, st, A, pause_at, max_steps);
+  const size_t lds = sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * SV_COUNT * A.Dp);
+  if (lds > 64 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)k_nuts_fused_schools<NCH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+  }
+  hipLaunchKernelGGL(k_nuts_fused_schools<NCH>, dim3(A.nchains), dim3(64), lds, st, A, pause_at, max_steps);
   return hipGetLastError();
 }
 
