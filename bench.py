@@ -163,7 +163,10 @@ def main():
         if its.min() >= A:
             break
     t_adapt = time.perf_counter() - t
+    t = time.perf_counter()
     sampler.run(total, max_steps=W)
+    ctx.sync()
+    t_wsteps = time.perf_counter() - t
     log(f"warmup steps done; timing {K} steps")
 
     def barrier():
@@ -340,6 +343,7 @@ def main():
         "ess_method": "min over parameters (lp__ excluded) of the consensus draws completed in the timed window; "
                       "sum over rank-paired chains of Stan's single-chain ESS",
         "ess_per_sec_equal_length": (ess_eq / elapsed) if ess_eq else None,
+        "ess_per_sec_incl_warmup": (min_ess / (t_adapt + t_wsteps + elapsed)) if min_ess else None,
         "subposterior_min_ess_shard0": sub_ess,
         "consensus_vs_generating_params": truth_check,
         "transitions_per_chain_in_window": {"min": int(done_in_window.min()), "median": float(np.median(done_in_window)),
