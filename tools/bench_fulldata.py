@@ -21,6 +21,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -36,6 +38,10 @@ def main():
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--seed", type=int, default=20240)
+    p.add_argument("--init-radius", type=float, default=2.0, help="pystan init_r (Stan default 2)")
+    p.add_argument("--adapt-iters", type=int, default=0,
+                   help="> 0: run Stan's warmup (untimed) first and report ESS/s of the transitions the "
+                        "chains complete inside the timed window")
     a = p.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -61,11 +67,27 @@ def main():
     ctx.sync()
     t_gen = time.perf_counter() - t
     K, W = a.steps, a.warmup
-    fs = fulldata.FullDataSampler(model, num_warmup=1000, num_samples=100, chains=a.chains, seed=a.seed + 1)
+    A = a.adapt_iters
+    nw = A if A > 0 else 1000
+    total = nw + K + W + 1
+    fs = fulldata.FullDataSampler(model, num_warmup=nw, num_samples=total - nw, chains=a.chains, seed=a.seed + 1,
+                                  stepsize_jitter=0.5 if A > 0 else 0.0, init_radius=a.init_radius)
     if rank == 0:
         print(f"[bench_fulldata] {world} GPU(s) x {rows} rows x d={a.d}: {model.device_bytes() / 1e9:.1f} GB/GPU, "
               f"generated in {t_gen:.1f}s", file=sys.stderr, flush=True)
-    fs.run(1100, max_steps=W)
+    t_adapt = 0.0
+    if A > 0:
+        t = time.perf_counter()
+        while True:                                   # bounded batches: a progress line per batch
+            fs.run(A, max_steps=500)
+            its = fs.iterations()
+            if rank == 0:
+                print(f"[bench_fulldata] warmup: {time.perf_counter() - t:.1f}s, transitions min/median "
+                      f"{its.min()}/{int(np.median(its))} of {A}", file=sys.stderr, flush=True)
+            if its.min() >= A:
+                break
+        t_adapt = time.perf_counter() - t
+    fs.run(total, max_steps=W)
 
     def barrier():
         torch.cuda.synchronize(local_rank)
@@ -74,18 +96,37 @@ def main():
 
     ctx.set_profiling(True)
     i0 = fs.info()
+    it0 = fs.iterations()
     barrier()
     t0 = time.perf_counter()
-    fs.run(1100, max_steps=K)
+    fs.run(total, max_steps=K)
     ctx.sync()
     barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_profiling(False)
     i1 = fs.info()
+    it1 = fs.iterations()
+    ess_ps, min_ess = None, None
+    if A > 0 and rank == 0:
+        # window transitions of every chain (ragged), ESS = min over parameters (lp__ excluded)
+        # of the sum over chains of Stan's single-chain estimator
+        from stark_amd import diagnostics
+        dr, _ = fs.draws(0)
+        per = total - nw
+        done = it1 - it0
+        es = np.zeros(dr.shape[0] - 1)
+        for c in range(a.chains):
+            f0 = it0[c] - nw
+            if done[c] >= 4:
+                seg = dr[:-1, c * per + f0: c * per + f0 + done[c]]
+                es += np.array([diagnostics.ess(seg[j]) for j in range(seg.shape[0])])
+        min_ess = float(np.nanmin(es)) if es.any() else None
     if world > 1:
         v = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local_rank))
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         elapsed = float(v.item())
+    if min_ess:
+        ess_ps = min_ess / elapsed
     steps = i1["steps"] - i0["steps"]
     grads = i1["grad_evals"] - i0["grad_evals"]      # chain-gradients of the full data set (same on every rank)
     sweeps = i1["sweeps"] - i0["sweeps"]
@@ -103,14 +144,16 @@ def main():
                    "rows_total": rows * world, "rows_per_gpu": rows, "d": a.d, "chains": a.chains,
                    "parallelism": f"row-dp{world}", "note": "N=1e9 (8 TB) exceeds node HBM; rows per GPU resident"},
         "rows_x_chains_per_sec": grads * rows * world / elapsed,
-        "ess_per_sec": None,
+        "ess_per_sec": ess_ps, "min_ess": min_ess, "adapt_iters": A,
+        "transitions_in_window": ({"min": int((it1 - it0).min()), "median": float(np.median(it1 - it0))}
+                                  if A > 0 else None),
         "roofline": {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": tfs / FP64_PEAK_TFS, "traffic": None,
                      "kernel": "k_gemm_fwd + k_gemm_bwd (fp64 MFMA 16x16x4, 64 chains)", "avg_launch_ms": avg_ms,
                      "algorithmic_flops_per_launch": flops,
                      "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
                              "algorithmic_bytes_per_launch": hbm_bytes}},
-        "setup_s": {"datagen": t_gen},
+        "setup_s": {"datagen": t_gen, "adaptation": t_adapt},
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
