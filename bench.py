@@ -284,7 +284,7 @@ def main():
     # C = 16: k_sweepm, X.[beta_1..beta_16] on fp64 MFMA, bound by the fp64 pipe;
     # C <= 4: k_sweep3 (VALU), bound by HBM.
     mfma = a.chains == 16
-    kname = "k_sweepm" if mfma else "k_sweep3"
+    kname = ("k_sweepe" if a.d == 100 else "k_sweepm") if mfma else "k_sweep3"
     ybytes = 4 if a.family == "logistic" else 8
     fam = "LOGREG" if a.family == "logistic" else "LINREG"
     bytes_per_shard = rows_per_shard * (8 * a.d + ybytes)   # X fp64 + y (int32 / fp64), once per sweep
@@ -309,7 +309,7 @@ def main():
     if mfma:
         roof = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": (tfs / FP64_PEAK_TFS) if tfs else None, "traffic": traffic,
-                "kernel": f"k_sweepm<{fam}> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
+                "kernel": f"{kname}<{fam}> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
                 "algorithmic_flops_per_launch": flops_per_launch, "algorithmic_bytes_per_launch": bytes_per_launch,
                 "hbm": hbm, "fp64_measured_ceiling_tfs": FP64_MEASURED_TFS}
     else:
