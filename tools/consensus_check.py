@@ -26,7 +26,10 @@ ctx = engine.Context(0)
 rps = int(a.rows) // a.shards
 m = engine.Model.synthetic(ctx, "logistic", a.shards, rps, a.d, data_seed=a.seed)
 s = m.sampler(num_warmup=a.warmup, num_samples=a.samples, chains=a.chains, seed=a.seed + 1, stepsize_jitter=a.jitter)
-s.run()
+total = a.warmup + a.samples
+for t in list(range(50, total, 50)) + [total]:     # resumable run: a progress line per 50 transitions
+    s.run(t)
+    print(f"[consensus_check] {t}/{total} transitions per chain", file=sys.stderr, flush=True)
 truth = np.concatenate([[0.0], engine.Model.gen_beta(a.seed, a.d)])
 draws = [s.draws(k)[0] for k in range(a.shards)]
 out = {"config": vars(a), "shards": []}
