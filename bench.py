@@ -254,7 +254,8 @@ def main():
     ess_ps, min_ess, ess_eq, sub_ess, truth_check = None, None, None, None, None
     if rank == 0 and Mk.sum() > P + 1 and Mk.max() >= 4:
         sub_ess = ess_rows(allp[0][:-1], False)
-        comb, used = engine.consensus(allp, ctx)
+        comb, used = engine.consensus(allp, ctx, separate_lp=True)
+        comb_joint, _ = engine.consensus(allp, ctx)                # the reference's joint weights (lp__ in)
         min_ess = ess_rows(comb[:-1], False)                     # drop lp__
         ess_eq = ess_rows(comb[:-1], True) if Mk.min() >= 4 else None
         ess_ps = min_ess / elapsed
@@ -265,11 +266,14 @@ def main():
             truth = np.concatenate([truth, [1.0]])             # sigma
         z = (comb[:-1].mean(axis=1) - truth) / comb[:-1].std(axis=1)
         zs = (allp[0][:-1].mean(axis=1) - truth) / allp[0][:-1].std(axis=1)
+        zj = (comb_joint[:-1].mean(axis=1) - truth) / comb_joint[:-1].std(axis=1)
         truth_check = {"max_abs_z": float(np.abs(z).max()), "mean_z2": float((z ** 2).mean()),
                        "subposterior_shard0_mean_z2": float((zs ** 2).mean()), "params": int(z.size),
-                       "note": "consensus weights inv(cov) are estimated from the window's draws "
-                               "(sum Mk per shard, P = d + 2): their noise, ~sqrt(P / draws), moves the combined "
-                               "mean (stark/stark.py:7-21 behaves the same); subposteriors alone have mean z^2 ~ 1"}
+                       "joint_lp_weights_mean_z2": float((zj ** 2).mean()),
+                       "note": "consensus with lp__ in its own weight block (engine.consensus separate_lp); "
+                               "joint_lp_weights_mean_z2 = the reference's joint combine (lp__ inside inv(cov), "
+                               "stark/stark.py:49-56), where each shard's lp__ offset leaks into the parameters "
+                               "through the sampled cross-covariances (DESIGN.md section 8)"}
     info = sampler.info()
     sampler.close()
 

@@ -401,10 +401,22 @@ def _stack(draws):
     return np.ascontiguousarray(np.stack(d)), d[0].shape
 
 
-def consensus(draws, ctx: Context | None = None):
+def consensus(draws, ctx: Context | None = None, separate_lp: bool = False):
     """(sum_s W_s)^-1 sum_s W_s theta_s, W_s = inv(cov(theta_s)): stark/stark.py:66-70 over
-    the reducer stark/stark.py:7-21.  Returns (P x S, shard_used)."""
+    the reducer stark/stark.py:7-21.  Returns (P x S, shard_used).
+
+    separate_lp: the last row (lp__, which fit.extract() hands the reference's combine,
+    stark/stark.py:49-56) gets a 1 x 1 weight block of its own instead of joining the parameter
+    rows' covariance.  Each shard's lp__ sits at its own offset, many of its sds apart; with a
+    sample covariance, the noise in the lp__-parameter cross terms moves the parameter rows of
+    the joint combine by a multiple of that offset.  Block weights are exact for a Gaussian
+    posterior, where lp__ is uncorrelated with the parameters."""
     ctx = ctx or default_context()
+    if separate_lp:
+        d = [np.asarray(x, np.float64) for x in draws]
+        th, used_t = consensus([x[:-1] for x in d], ctx)
+        lp, _ = consensus([x[-1:] for x in d], ctx)
+        return np.vstack([th, lp]), used_t
     X, (P, S) = _stack(draws)
     out = np.empty((P, S))
     used = np.empty(len(draws), np.int32)

@@ -200,12 +200,15 @@ class Stark:
         local = dict(zip(mine, self._sample_partitions(datas, shard_ids=mine, **kwargs))) if datas else {}
         return dist.all_gather_partitions(local, len(parts))
 
-    def concensusWeight(self, **kwargs):
-        """stark/stark.py:59-71: subposterior per partition, consensus weighted average."""
+    def concensusWeight(self, separate_lp=False, **kwargs):
+        """stark/stark.py:59-71: subposterior per partition, consensus weighted average.
+        The default combines every extract() row jointly, lp__ included, as the reference does;
+        separate_lp=True gives lp__ its own weight block so the parameter rows are combined
+        from the parameters' covariance alone (engine.consensus)."""
         kwargs = self._defaults(kwargs)
         parts = _rdd.partitions_of(self.rdd)
         subposteriors = self._run_distributed(parts, **kwargs)
-        out, _ = engine.consensus(subposteriors)
+        out, _ = engine.consensus(subposteriors, separate_lp=separate_lp)
         return out
 
     def distribute(self, n=2, reference_union=False, **kwargs):

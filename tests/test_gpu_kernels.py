@@ -141,6 +141,36 @@ def test_combine_general_shards(ctx, orc, S):
                                    atol=1e-11 * np.abs(ref).max())
 
 
+def test_combine_separate_lp(ctx, orc):
+    """engine.consensus(separate_lp=True): parameter rows and the lp__ row are combined as two
+    weight blocks (each = the oracle combine of that block alone); with shard lp__ offsets of
+    300 lp-sds, the joint combine (the reference's, stark/stark.py:49-56) moves the parameter
+    means by several posterior sds, the block combine does not.  Gaussian shards, so the exact
+    full-data mean is the average of the shard means."""
+    from stark_amd import engine
+    rng = np.random.default_rng(11)
+    P, n, S = 21, 1000, 8
+    A = rng.normal(size=(P, P)) / np.sqrt(P)
+    L = np.linalg.cholesky(8 * (A @ A.T + 0.5 * np.eye(P)))
+    mus = [L @ rng.normal(size=P) for _ in range(S)]
+    draws = []
+    for s in range(S):
+        w = rng.normal(size=(P, n))
+        lp = -0.5 * (w ** 2).sum(0) + 300 * np.sqrt(P / 2) * rng.normal()
+        draws.append(np.vstack([mus[s][:, None] + L @ w, lp]))
+    out, used = engine.consensus(draws, ctx, separate_lp=True)
+    assert used.all() and out.shape == (P + 1, n)
+    ref_t = orc.consensus_combine_ref([d[:-1] for d in draws])
+    ref_l = orc.consensus_combine_ref([d[-1:] for d in draws])
+    np.testing.assert_allclose(out[:-1], ref_t, rtol=1e-10, atol=1e-11 * np.abs(ref_t).max())
+    np.testing.assert_allclose(out[-1:], ref_l, rtol=1e-10, atol=1e-11 * np.abs(ref_l).max())
+    joint, _ = engine.consensus(draws, ctx)
+    full = np.mean(mus, axis=0)
+    z2 = lambda c: float((((c.mean(1) - full) / c.std(1)) ** 2).mean())
+    assert z2(out[:-1]) < 0.2          # weight noise alone: ~P / n per shard (measured 0.009)
+    assert z2(joint[:-1]) > 5.0        # lp__ offsets leak through the cross-covariances (measured 38.6)
+
+
 def test_combine_singular_raises(ctx):
     from stark_amd import engine
     from stark_amd._lib import LinAlgError

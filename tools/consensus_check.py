@@ -41,6 +41,11 @@ for k, dr in enumerate(draws):
 comb, used = engine.consensus(draws, ctx)
 z = (comb[:-1].mean(1) - truth) / comb[:-1].std(1)
 out["consensus"] = {"max_abs_z": float(np.abs(z).max()), "mean_z2": float((z ** 2).mean())}
+comb_b, _ = engine.consensus(draws, ctx, separate_lp=True)     # lp__ in its own weight block
+zb = (comb_b[:-1].mean(1) - truth) / comb_b[:-1].std(1)
+out["consensus_separate_lp"] = {"max_abs_z": float(np.abs(zb).max()), "mean_z2": float((zb ** 2).mean())}
+lpm = np.array([dr[-1].mean() for dr in draws])
+out["lp_offsets_over_sd"] = float(lpm.std() / np.mean([dr[-1].std() for dr in draws]))
 # the consensus mean vs the average of the subposterior means (should agree to within sd/sqrt(S))
 sub_mean = np.mean([dr[:-1].mean(1) for dr in draws], axis=0)
 out["consensus_minus_submean_over_sd"] = float(np.abs((comb[:-1].mean(1) - sub_mean) / comb[:-1].std(1)).max())
