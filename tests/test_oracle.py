@@ -36,6 +36,26 @@ def test_combine_restatement_matches_reference(golden, orc, P):
     np.testing.assert_allclose(final, g[f"P{P}_final"], rtol=1e-9, atol=1e-12 * np.abs(final).max())
 
 
+def test_combine_lp_row_leak(orc):
+    """The reference's joint combine (lp__ inside inv(cov), stark/stark.py:49-56) on Gaussian
+    shards whose lp__ rows sit 300 lp-sds apart: the parameter means move by several posterior
+    sds; combining the parameter rows alone (the separate_lp block) does not."""
+    rng = np.random.default_rng(11)
+    P, n, S = 21, 1000, 8
+    A = rng.normal(size=(P, P)) / np.sqrt(P)
+    L = np.linalg.cholesky(8 * (A @ A.T + 0.5 * np.eye(P)))
+    mus = [L @ rng.normal(size=P) for _ in range(S)]
+    draws = []
+    for s in range(S):
+        w = rng.normal(size=(P, n))
+        lp = -0.5 * (w ** 2).sum(0) + 300 * np.sqrt(P / 2) * rng.normal()
+        draws.append(np.vstack([mus[s][:, None] + L @ w, lp]))
+    full = np.mean(mus, axis=0)
+    z2 = lambda c: float((((c.mean(1) - full) / c.std(1)) ** 2).mean())
+    assert z2(orc.consensus_combine_ref(draws)[:-1]) > 5.0
+    assert z2(orc.consensus_combine_ref([d[:-1] for d in draws])) < 0.2
+
+
 def test_combine_nan_guard_reference(golden, orc):
     g = golden("combine_ref.npz")
     out = orc.consensus_avg_ref(g["nan_f1"], g["nan_f2"])
