@@ -161,7 +161,8 @@ def test_combine_separate_lp(ctx, orc):
     out, used = engine.consensus(draws, ctx, separate_lp=True)
     assert used.all() and out.shape == (P + 1, n)
     ref_t = orc.consensus_combine_ref([d[:-1] for d in draws])
-    ref_l = orc.consensus_combine_ref([d[-1:] for d in draws])
+    wl = [1.0 / np.var(d[-1], ddof=1) for d in draws]     # 1 x 1 blocks: inverse variances
+    ref_l = (sum(w * d[-1:] for w, d in zip(wl, draws)) / sum(wl))
     np.testing.assert_allclose(out[:-1], ref_t, rtol=1e-10, atol=1e-11 * np.abs(ref_t).max())
     np.testing.assert_allclose(out[-1:], ref_l, rtol=1e-10, atol=1e-11 * np.abs(ref_l).max())
     joint, _ = engine.consensus(draws, ctx)
