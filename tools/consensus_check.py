@@ -44,6 +44,13 @@ out["consensus"] = {"max_abs_z": float(np.abs(z).max()), "mean_z2": float((z ** 
 comb_b, _ = engine.consensus(draws, ctx, separate_lp=True)     # lp__ in its own weight block
 zb = (comb_b[:-1].mean(1) - truth) / comb_b[:-1].std(1)
 out["consensus_separate_lp"] = {"max_abs_z": float(np.abs(zb).max()), "mean_z2": float((zb ** 2).mean())}
+# is the excess in the subposteriors themselves?  mean over shards of the signed shard z,
+# times sqrt(S): ~N(0, 1) per parameter when the shards' errors are independent
+zsh = np.array([(dr[:-1].mean(1) - truth) / dr[:-1].std(1) for dr in draws])
+zc = zsh.mean(0) * np.sqrt(len(draws))
+out["shard_mean_z_times_sqrtS_mean_sq"] = float((zc ** 2).mean())
+out["shard_z_corr_with_beta"] = float(np.corrcoef(zsh.mean(0)[1:], truth[1:])[0, 1])
+out["consensus_err_corr_with_beta"] = float(np.corrcoef(zb[1:], truth[1:])[0, 1])
 lpm = np.array([dr[-1].mean() for dr in draws])
 out["lp_offsets_over_sd"] = float(lpm.std() / np.mean([dr[-1].std() for dr in draws]))
 # the consensus mean vs the average of the subposterior means (should agree to within sd/sqrt(S))
