@@ -9,17 +9,15 @@ every local shard, i.e. one leapfrog of every chain (chains share a shard's swee
 by the deterministic chunk reduction and one NUTS state-machine step.  Chains are never held
 back by each other: each runs its own trajectories, transitions and draws.  Timeline:
   data generated in HBM (Philox, not timed) -> Stan warmup with adaptation, --adapt-iters
-  transitions per chain (not timed) -> W untimed steps -> barrier+sync -> K timed steps ->
-  sync+barrier.
+  transitions per chain -> W untimed steps -> barrier+sync -> K timed steps -> sync+barrier
+  -> ESS phase: every chain runs on to the same number of post-warmup draws (--ess-draws)
+  -> one all-gather of the draws -> consensus combine on the GPU -> ESS.
 `value` = chain-gradient evaluations of all ranks in the timed region / max-over-ranks time
 (every chain evaluates one gradient per step, so = chains * K / time).
-ESS/s: the transitions every chain completed inside the timed window, rank-paired across
-shards (combined chain k = the chain with the k-th most window transitions of each shard,
-cut to the fewest of them, so draw i of every shard is combined with draw i of the others);
-the consensus combine runs on the GPU after one all-gather; ESS/s = min over non-lp__
-parameters of the combined draws' ESS (sum over combined chains of Stan's single-chain
-estimator) / the timed window.  ess_per_sec_equal_length: Stan's multi-chain estimator on
-every chain cut to the shortest (conservative).
+`ess_per_sec` = min over alpha, beta of Stan 2.19's multi-chain ESS of the
+consensus draws / the whole sampling wall time, adaptation included (data upload excluded).
+`accuracy` compares the consensus with the full-data posterior (MAP + inverse Hessian from
+the GPU gradient, tools/laplace.py) and with the data-generating parameters.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
 """
@@ -36,13 +34,12 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_PEAK_TFS = 78.6    # MI355X fp64 matrix (= vector) spec, dense
-FP64_MEASURED_TFS = 46.0  # v_mfma_f64_16x16x4 back to back, 2+ waves/SIMD (tools/mfma_overlap.hip, profiles/)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=4000)
+    p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--family", choices=["logistic", "linear"], default="logistic",
                    help="linear --rows 1e7 --d 50: BASELINE configs[2]")
@@ -56,6 +53,9 @@ def parse():
     p.add_argument("--stepsize-jitter", type=float, default=0.5,
                    help="Stan control stepsize_jitter; breaks the trajectory-length resonance of NUTS on "
                         "this near-isotropic posterior (DESIGN.md section 4)")
+    p.add_argument("--ess-draws", type=int, default=100,
+                   help="post-warmup draws per chain for the ESS / accuracy phase (after the timed steps)")
+    p.add_argument("--no-accuracy", action="store_true", help="skip the full-data Laplace reference")
     p.add_argument("--seed", type=int, default=20240)
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -82,6 +82,20 @@ def cpu_baseline(d, rows_per_shard, shards, seconds, family="logistic"):
                       f"(C, 1 thread/worker) on {sample_rows} rows x d={d} per worker, "
                       f"{seconds:.0f}s per worker, {workers} concurrent workers (one per shard, Spark local[*] model), "
                       f"scaled linearly to {rows_per_shard:.3g} rows/shard; analytic gradient (optimistic vs Stan autodiff)"}
+
+
+def cpu_combine(draws):
+    """The reference's combine arithmetic on the host (oracle.consensus_combine_ref: numpy
+    inv(np.cov) per shard, sums, inv(sum W) . sum W theta -- stark/stark.py:7-21, 66-70, the
+    reference's own operations), timed on the same draws as the GPU combine."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    d = [np.asarray(x[:-1]) for x in draws]
+    t = time.perf_counter()
+    O.consensus_combine_ref(d)
+    O.consensus_combine_ref([np.asarray(x[-1:]) for x in draws])
+    return {"combine_ms": 1e3 * (time.perf_counter() - t),
+            "combine_note": "numpy restatement of the reference combine (lp__ in its own block), 1 process"}
 
 
 def _cpu_worker(d, seconds, w, family="logistic"):
@@ -125,7 +139,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
-    from stark_amd import diagnostics, engine
+    from stark_amd import dist as sdist
+    from stark_amd import engine
 
     assert a.shards % world == 0, "shards must divide evenly over GPUs"
     spr = a.shards // world
@@ -140,14 +155,31 @@ def main():
     ctx.sync()
     t_gen = time.perf_counter() - t
 
-    A, W, K = a.adapt_iters, a.warmup, a.steps
-    total = A + W + K + 1          # enough sampling iterations that no chain finishes in the window
-    sampler = model.sampler(num_warmup=A, num_samples=total - A, chains=a.chains, seed=a.seed + 1,
+    A, W, K, ND = a.adapt_iters, a.warmup, a.steps, a.ess_draws
+    # every step is at most one transition per chain, so A + W + K + ND transitions always
+    # cover the timed window and the fixed post-warmup draws of the ESS phase
+    n_samp = W + K + ND + 1
+    sampler = model.sampler(num_warmup=A, num_samples=n_samp, chains=a.chains, seed=a.seed + 1,
                             shard_ids=shard_ids, stepsize_jitter=a.stepsize_jitter)
 
     def log(msg):
         if rank == 0:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    def barrier():
+        torch.cuda.synchronize(local_rank)
+        if dist:
+            dist.barrier()
+
+    def allreduce(arr, op="sum"):
+        """float64 numpy array summed (or maxed) over ranks in place (RCCL / gloo)."""
+        if not dist:
+            return arr
+        dev = sdist._device_for_backend()
+        t_ = torch.from_numpy(np.ascontiguousarray(arr, np.float64)).to(dev)
+        dist.all_reduce(t_, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        arr[...] = t_.cpu().numpy()
+        return arr
 
     log(f"data generated: {spr} shards x {rows_per_shard} rows x d={a.d} in {t_gen:.1f}s "
         f"({model.device_bytes() / 1e9:.1f} GB on this GPU)")
@@ -164,15 +196,10 @@ def main():
             break
     t_adapt = time.perf_counter() - t
     t = time.perf_counter()
-    sampler.run(total, max_steps=W)
+    sampler.run(A + n_samp, max_steps=W)
     ctx.sync()
     t_wsteps = time.perf_counter() - t
     log(f"warmup steps done; timing {K} steps")
-
-    def barrier():
-        torch.cuda.synchronize(local_rank)
-        if dist:
-            dist.barrier()
 
     nchains = spr * a.chains
     it0 = sampler.iterations()
@@ -180,7 +207,7 @@ def main():
     i0 = sampler.info()
     barrier()
     t0 = time.perf_counter()
-    sampler.run(total, max_steps=K)
+    sampler.run(A + n_samp, max_steps=K)
     ctx.sync()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -194,87 +221,44 @@ def main():
     shard_sweeps = i1["shard_sweeps"] - i0["shard_sweeps"]
     sweep_ms = i1["sweep_ms"] - i0["sweep_ms"]
     done_in_window = it1 - it0                       # transitions completed per chain
-    eps, _ = sampler.adaptation()
     if dist:
-        v = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local_rank))
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        elapsed = float(v.item())
-        g = torch.tensor([grads, leaps], dtype=torch.float64, device=torch.device("cuda", local_rank))
-        dist.all_reduce(g, op=dist.ReduceOp.SUM)
-        grads, leaps = int(g[0].item()), int(g[1].item())
+        elapsed = float(allreduce(np.array([elapsed]), "max")[0])
+        grads, leaps = (int(v) for v in allreduce(np.array([grads, leaps], np.float64)))
 
-    # ---- draws completed inside the window -> consensus -> ESS.
-    # The consensus average pairs draw i of every shard; chains are exchangeable, so combined
-    # chain k joins the chain with the k-th most window transitions of every shard and keeps
-    # M_k = the fewest of those (no draw is made up, chain boundaries align across shards).
-    C = a.chains
-    P = model.P[0]
-    counts = {shard_ids[s]: done_in_window[s * C:(s + 1) * C].astype(int).tolist() for s in range(spr)}
-    if dist:
-        gathered = [None] * world
-        dist.all_gather_object(gathered, counts)
-        counts = {k_: v_ for dct in gathered for k_, v_ in dct.items()}
-    order = {sh: np.argsort(-np.asarray(cnt), kind="stable") for sh, cnt in counts.items()}
-    Mk = np.array([min(counts[sh][order[sh][k]] for sh in counts) for k in range(C)])
-    local = {}
-    per = total - A
-    for s in range(spr):
-        dr, _ = sampler.draws(s)
-        sh = shard_ids[s]
-        cols = []
-        for k in range(C):
-            c = order[sh][k]
-            first = it0[s * C + c] - A               # sampling index of the chain's first window transition
-            cols.append(np.arange(c * per + first, c * per + first + Mk[k]))
-        local[sh] = np.ascontiguousarray(dr[:, np.concatenate(cols)]) if Mk.sum() > 0 else None
-    if dist:
-        allp = [None] * a.shards
-        gathered = [None] * world
-        dist.all_gather_object(gathered, local)
-        for dct in gathered:
-            for k_, v_ in dct.items():
-                allp[k_] = v_
-    else:
-        allp = [local[k_] for k_ in range(a.shards)]
-
-    def ess_rows(x, equal):
-        """min over parameter rows of the ESS of x (P' x sum(Mk), chain segments of lengths Mk):
-        equal: Stan's multi-chain estimator on every segment cut to min(Mk);
-        else: sum over segments (M_k >= 4) of Stan's single-chain estimator (independent chains)."""
-        off = np.concatenate([[0], np.cumsum(Mk)])
-        out = []
-        for p in range(x.shape[0]):
-            if equal:
-                m = int(Mk.min())
-                out.append(diagnostics.ess(np.stack([x[p, off[k]:off[k] + m] for k in range(C)])))
-            else:
-                out.append(sum(diagnostics.ess(x[p, off[k]:off[k + 1]]) for k in range(C) if Mk[k] >= 4))
-        return float(np.nanmin(out))
-
-    ess_ps, min_ess, ess_eq, sub_ess, truth_check = None, None, None, None, None
-    if rank == 0 and Mk.sum() > P + 1 and Mk.max() >= 4:
-        sub_ess = ess_rows(allp[0][:-1], False)
-        comb, used = engine.consensus(allp, ctx, separate_lp=True)
-        comb_joint, _ = engine.consensus(allp, ctx)                # the reference's joint weights (lp__ in)
-        min_ess = ess_rows(comb[:-1], False)                     # drop lp__
-        ess_eq = ess_rows(comb[:-1], True) if Mk.min() >= 4 else None
-        ess_ps = min_ess / elapsed
-        # large-scale sanity of the combined posterior: the generating (alpha = 0, beta) lies
-        # within a few posterior sd of the consensus mean (z ~ N(0, 1) per parameter)
-        truth = np.concatenate([[0.0], engine.Model.gen_beta(a.seed, a.d)])
-        if a.family == "linear":
-            truth = np.concatenate([truth, [1.0]])             # sigma
-        z = (comb[:-1].mean(axis=1) - truth) / comb[:-1].std(axis=1)
-        zs = (allp[0][:-1].mean(axis=1) - truth) / allp[0][:-1].std(axis=1)
-        zj = (comb_joint[:-1].mean(axis=1) - truth) / comb_joint[:-1].std(axis=1)
-        truth_check = {"max_abs_z": float(np.abs(z).max()), "mean_z2": float((z ** 2).mean()),
-                       "subposterior_shard0_mean_z2": float((zs ** 2).mean()), "params": int(z.size),
-                       "joint_lp_weights_mean_z2": float((zj ** 2).mean()),
-                       "note": "consensus with lp__ in its own weight block (engine.consensus separate_lp); "
-                               "joint_lp_weights_mean_z2 = the reference's joint combine (lp__ inside inv(cov), "
-                               "stark/stark.py:49-56), where each shard's lp__ offset leaks into the parameters "
-                               "through the sampled cross-covariances (DESIGN.md section 8)"}
+    # ---- ESS phase (not part of `value`): every chain of every rank runs on to the same
+    # number of post-warmup draws, n_post = max(ND, the most any chain already has), so the
+    # consensus pairs draw i of chain c of every shard (equal-length chains, Stan's
+    # multi-chain estimator).  Its time counts in the ESS/s denominators.
+    n_post = int(allreduce(np.array([max(ND, int(it1.max()) - A)], np.float64), "max")[0])
+    t = time.perf_counter()
+    sampler.run(A + n_post)
+    ctx.sync()
+    barrier()
+    t_post = time.perf_counter() - t
     info = sampler.info()
+    C = a.chains
+    local = {}
+    stats = []
+    for s in range(spr):
+        dr, st = sampler.draws(s)
+        cols = np.concatenate([np.arange(c * n_samp, c * n_samp + n_post) for c in range(C)])
+        local[shard_ids[s]] = np.ascontiguousarray(dr[:, cols])
+        stats.append(st[cols])
+    stats = np.vstack(stats)
+    t = time.perf_counter()
+    allp = sdist.all_gather_partitions(local, a.shards)       # one all-gather (RCCL on GPUs)
+    t_gather = time.perf_counter() - t
+    eps, _ = sampler.adaptation()
+    # full-data posterior reference (logistic, flat priors): MAP + inverse Hessian from the
+    # GPU gradient summed over every shard of every rank (tools/laplace.py)
+    lap = None
+    if a.family == "logistic" and not a.no_accuracy:
+        from tools import laplace as L
+        t = time.perf_counter()
+        pooled = np.hstack([x[:-1] for x in allp])
+        lap = L.laplace(model, list(range(spr)), pooled.mean(1), pooled.std(1) / np.sqrt(a.shards),
+                        reduce=(lambda arr: allreduce(arr)) if dist else None)
+        log(f"full-data Laplace reference in {time.perf_counter() - t:.1f}s")
     sampler.close()
 
     if rank != 0:
@@ -283,6 +267,44 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
+
+    from stark_amd import diagnostics
+    P = allp[0].shape[0]
+    t = time.perf_counter()
+    comb, used = engine.consensus(allp, ctx, separate_lp=True)
+    t_comb = time.perf_counter() - t
+    comb_joint, _ = engine.consensus(allp, ctx)               # the reference's joint weights (lp__ in)
+
+    def min_ess(x):
+        return float(np.nanmin([diagnostics.ess(x[p].reshape(C, n_post)) for p in range(x.shape[0])]))
+
+    ess_c = min_ess(comb[:-1])                                 # lp__ excluded
+    ess_s0 = min_ess(allp[0][:-1])
+    t_sampling = t_wsteps + elapsed + t_post
+    truth = np.concatenate([[0.0], engine.Model.gen_beta(a.seed, a.d)])
+    if a.family == "linear":
+        truth = np.concatenate([truth, [1.0]])                # sigma
+    csd = comb[:-1].std(1)
+
+    def zz(err, sd):
+        z = err / sd
+        return {"mean_z2": float((z ** 2).mean()), "max_abs_z": float(np.abs(z).max())}
+
+    accuracy = {"vs_generating_params": zz(comb[:-1].mean(1) - truth, csd),
+                "vs_generating_params_joint_lp": zz(comb_joint[:-1].mean(1) - truth, csd)}
+    if lap is not None:
+        fm, fc, finfo = lap
+        fsd = np.sqrt(np.diag(fc))
+        accuracy["vs_fulldata_laplace"] = {
+            "consensus": zz(comb[:-1].mean(1) - fm, fsd),
+            "consensus_joint_lp": zz(comb_joint[:-1].mean(1) - fm, fsd),
+            "sd_ratio_median": float(np.median(csd / fsd)),
+            "truth": zz(truth - fm, fsd),
+            "newton_steps_in_sd": finfo["newton_steps_in_sd"]}
+    accuracy["note"] = ("z = (mean - reference) / reference sd per parameter over all alpha, beta; the consensus "
+                        "puts lp__ in its own weight block (engine.consensus separate_lp); *_joint_lp = the "
+                        "reference's joint combine (lp__ inside inv(cov), stark/stark.py:49-56). vs_fulldata_laplace: "
+                        "the full-data posterior (MAP + inverse Hessian of the GPU gradient, tools/laplace.py)")
 
     # ---- roofline of the dominant kernel (the data sweep)
     # C = 16: k_sweepm, X.[beta_1..beta_16] on fp64 MFMA, bound by the fp64 pipe;
@@ -315,16 +337,22 @@ def main():
                 "frac": (tfs / FP64_PEAK_TFS) if tfs else None, "traffic": traffic,
                 "kernel": f"{kname}<{fam}> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
                 "algorithmic_flops_per_launch": flops_per_launch, "algorithmic_bytes_per_launch": bytes_per_launch,
-                "hbm": hbm, "fp64_measured_ceiling_tfs": FP64_MEASURED_TFS}
+                "hbm": hbm}
     else:
         roof = dict(bound="hbm", **{k: v for k, v in hbm.items()}, traffic=traffic,
                     kernel=f"k_sweep3<{fam},{a.chains}>", avg_launch_ms=avg_ms,
                     algorithmic_bytes_per_launch=bytes_per_launch)
+    value = grads / elapsed
+    # ESS per gradient evaluation of the whole run (warmup included): the same algorithm on the
+    # CPU twin (transition-identical, tests/test_gpu_nuts.py) spends the same gradients per ESS
+    total_grads = info["grad_evals"] * world
     cpu = None
     if not a.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(a.d, rows_per_shard, a.shards, a.cpu_baseline_seconds, a.family)
-
-    value = grads / elapsed
+        cpu["ess_per_sec"] = cpu["value"] * ess_c / total_grads
+        cpu["ess_note"] = ("the measured CPU gradient rate x this run's ESS per gradient evaluation "
+                           "(warmup included): the CPU twin runs the same NUTS transitions")
+        cpu.update(cpu_combine(allp))
     line = {
         "metric": f"gradient evals/sec (whole node), {a.family} regression N={a.rows:.0e} d={a.d}".replace("e+0", "e"),
         "value": value,
@@ -340,25 +368,28 @@ def main():
         "data": "synthetic (Philox in HBM, SURVEY 8d)",
         "config": {"workload": f"bayesian {a.family} regression, {a.shards} subposterior shards + consensus combine",
                    "rows": int(a.rows), "d": a.d, "shards": a.shards, "shards_per_gpu": spr,
-                   "chains_per_shard": a.chains, "adapt_iters": A, "stepsize_jitter": a.stepsize_jitter,
-                   "parallelism": f"shard-dp{world}"},
-        "ess_per_sec": ess_ps,
-        "min_ess": min_ess,
-        "ess_method": "min over parameters (lp__ excluded) of the consensus draws completed in the timed window; "
-                      "sum over rank-paired chains of Stan's single-chain ESS",
-        "ess_per_sec_equal_length": (ess_eq / elapsed) if ess_eq else None,
-        "ess_per_sec_incl_warmup": (min_ess / (t_adapt + t_wsteps + elapsed)) if min_ess else None,
-        "subposterior_min_ess_shard0": sub_ess,
-        "consensus_vs_generating_params": truth_check,
-        "transitions_per_chain_in_window": {"min": int(done_in_window.min()), "median": float(np.median(done_in_window)),
-                                            "max": int(done_in_window.max()), "used_for_ess": int(Mk.sum()),
-                                            "used_equal_length": int(C * Mk.min())},
+                   "chains_per_shard": a.chains, "num_warmup": A, "post_warmup_draws_per_chain": n_post,
+                   "stepsize_jitter": a.stepsize_jitter, "parallelism": f"shard-dp{world}"},
+        "ess_per_sec": ess_c / (t_adapt + t_sampling),
+        "min_ess": ess_c,
+        "ess_method": ("min over alpha, beta (lp__ excluded) of Stan 2.19's multi-chain ESS of the consensus draws "
+                       f"({C} combined chains x {n_post} post-warmup draws; combined chain c = chain c of every "
+                       "shard), divided by the whole sampling wall time: warmup/adaptation + the timed steps + the "
+                       "post-warmup draws (SURVEY 8d; data generation excluded)"),
+        "ess_per_sec_post_warmup": ess_c / t_sampling,
+        "num_warmup_note": (f"num_warmup = {A} (Stan's default iter=2000 would warm up for 1000; DESIGN.md 4): "
+                            "the adaptation is the dominant ESS/s cost"),
+        "subposterior_min_ess_shard0": ess_s0,
+        "accuracy": accuracy,
         "stepsize_per_chain": {"min": float(eps.min()), "median": float(np.median(eps)), "max": float(eps.max())},
-        "leapfrogs_per_transition": float(nchains * K / max(1, done_in_window.sum())),
+        "treedepth_mean": float(stats[:, 2].mean()),
+        "leapfrogs_per_transition": float(stats[:, 3].mean()),
         "rows_x_chains_per_sec": grads * rows_per_shard / elapsed,
         "roofline": roof,
         "cpu_baseline": cpu,
-        "setup_s": {"datagen": t_gen, "adaptation": t_adapt},
+        "combine": {"gpu_ms": 1e3 * t_comb, "shards": a.shards, "P": P, "draws": C * n_post,
+                    "all_gather_ms": 1e3 * t_gather},
+        "setup_s": {"datagen": t_gen, "adaptation": t_adapt, "post_warmup_draws": t_post},
         "divergent": info["divergent"],
     }
     print(json.dumps(line), flush=True)

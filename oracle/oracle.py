@@ -286,6 +286,38 @@ def schools_exact_moments(y, sigma, n_mu=1601, n_logtau=1601):
     return np.array(out_mean), np.array(out_var)
 
 
+def schools_exact_extract_means(y, sigma, n_mu=1601, n_logtau=1601):
+    """Posterior means of the 2J+3 rows fit.extract() gives for example/schools.stan, in
+    order: mu, tau, eta[1..J], theta[1..J], lp__ (the 19 "targets" of test/stark_test.py:26
+    for J = 8).  Same quadrature as schools_exact_moments; given (mu, tau) eta_j is normal
+    with mean em_j and variance ev_j, so theta_j = mu + tau eta_j and
+    lp__ = -sum eta^2 / 2 - sum ((y - theta) / sigma)^2 / 2 + log tau (Stan's log_prob,
+    propto, Jacobian of tau > 0) have closed-form conditional means."""
+    y = np.asarray(y, np.float64)
+    s2 = np.asarray(sigma, np.float64) ** 2
+    mus = np.linspace(-60, 80, n_mu)
+    us = np.linspace(-12, 6.5, n_logtau)
+    MU, U = np.meshgrid(mus, us, indexing="ij")
+    T2 = np.exp(2 * U)
+    tau = np.exp(U)
+    logp = U.copy()
+    for yj, sj2 in zip(y, s2):
+        var = sj2 + T2
+        logp += -0.5 * np.log(var) - 0.5 * (yj - MU) ** 2 / var
+    w = np.exp(logp - logp.max())
+    w /= w.sum()
+    mean_eta, mean_theta = [], []
+    lp = U.copy()
+    for yj, sj2 in zip(y, s2):
+        vj = 1.0 / (1.0 / T2 + 1.0 / sj2)
+        mj = vj * (MU / T2 + yj / sj2)
+        em, ev = (mj - MU) / tau, vj / T2
+        mean_eta.append((w * em).sum())
+        mean_theta.append((w * mj).sum())
+        lp += -0.5 * (ev + em * em) - 0.5 * ((yj - mj) ** 2 + vj) / sj2
+    return np.array([(w * MU).sum(), (w * tau).sum()] + mean_eta + mean_theta + [(w * lp).sum()])
+
+
 def linreg_exact_moments(X, y):
     """Flat-prior linear regression with sigma = exp(u), Jacobian u, i.e. p(sigma) flat:
     the marginal posterior of (alpha, beta) is multivariate t with nu = N - k - 1 dof

@@ -717,11 +717,11 @@ template <int NCH>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
   const size_t lds = sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * SV_COUNT * A.Dp);
   if (lds > 64 * 1024) {
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute((const void*)k_nuts_fused_schools<NCH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
+    // the attribute is per device: set it on every launch that needs it (a host call, once per
+    // fused launch of up to max_steps leapfrogs) and report a failure as such
+    const hipError_t e = hipFuncSetAttribute((const void*)k_nuts_fused_schools<NCH>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_nuts_fused_schools<NCH>, dim3(A.nchains), dim3(64), lds, st, A, pause_at, max_steps);
   return hipGetLastError();

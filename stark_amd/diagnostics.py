@@ -1,10 +1,13 @@
 """Sampler diagnostics: effective sample size and split R-hat.
 
-Restates Stan's ``stan::analyze::compute_effective_sample_size`` (Geyer initial positive +
-initial monotone sequence on the multi-chain autocovariance, with the antithetic
-correction of later 2.x releases) and ``compute_split_potential_scale_reduction`` -- the
-numbers ``stansummary`` reports.  Host-side reporting only; not on
-the hot path.
+Restates Stan 2.19.1's ``stan::analyze::compute_effective_sample_size`` (Geyer initial
+positive + initial monotone sequence on the multi-chain autocovariance, with the
+improved-tail term ``rho_hat_s(max_s + 1)`` that 2.19 already has) and
+``compute_split_potential_scale_reduction`` -- the numbers pystan 2.19 / ``stansummary``
+report.  Stan 2.19 has no lower bound on tau_hat; the
+``tau_hat >= 1 / log10(total draws)`` floor of later releases is available as
+``ess(..., floor=True)`` and is off by default.  Host-side reporting only; not on the hot
+path.
 """
 from __future__ import annotations
 
@@ -21,8 +24,9 @@ def _autocovariance(x: np.ndarray) -> np.ndarray:
     return ac / n
 
 
-def ess(chains) -> float:
-    """ESS of one scalar quantity; `chains` is (num_chains, num_draws)."""
+def ess(chains, floor: bool = False) -> float:
+    """ESS of one scalar quantity; `chains` is (num_chains, num_draws).
+    floor: apply the later releases' tau_hat >= 1/log10(N) bound (not in Stan 2.19)."""
     chains = np.atleast_2d(np.asarray(chains, np.float64))
     nc, n = chains.shape
     if n < 4:
@@ -57,8 +61,8 @@ def ess(chains) -> float:
             rho[t + 1] = (rho[t - 1] + rho[t]) / 2.0
             rho[t + 2] = rho[t + 1]
     tau = -1.0 + 2.0 * rho[:max_s].sum() + rho[max_s + 1]
-    # guard for very short / antithetic chains, as later Stan releases do
-    tau = max(tau, 1.0 / np.log10(nc * n))
+    if floor:
+        tau = max(tau, 1.0 / np.log10(nc * n))
     return float(nc * n / tau)
 
 

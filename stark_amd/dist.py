@@ -27,44 +27,54 @@ def local_partitions(n_partitions: int, rank: int, world_size: int):
 
 
 def _device_for_backend():
+    """RCCL ('nccl') collectives run on this rank's GPU (LOCAL_RANK); the object collectives
+    use torch's CURRENT device, so it is set here too -- otherwise every rank would send on
+    cuda:0."""
     import torch
     import torch.distributed as dist
     if dist.get_backend() == "nccl":
         import os
-        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(dev)
+        return dev
     return torch.device("cpu")
 
 
 def all_gather_partitions(local: dict, n_partitions: int):
-    """local: {partition index: 2-D float64 array}.  Returns the list over all partitions
-    (one all_gather of a padded [slots, rows, cols] fp64 tensor per rank)."""
+    """local: {partition index: 2-D float64 array} -- whatever partitions this rank holds
+    (round-robin p % world for the driver, contiguous blocks for bench.py).  Returns the
+    list over all partitions: one all_gather of a padded [slots, rows, cols] fp64 tensor per
+    rank, after a tiny object collective that tells every rank who holds which partition."""
     rank, ws = world()
-    if ws == 1:
+    import torch.distributed as _d
+    if not (_d.is_available() and _d.is_initialized()):
         return [local[p] for p in range(n_partitions)]
+    # an initialised group runs the collective even at world size 1 (same code path as N > 1)
     import torch
     import torch.distributed as dist
-    dev = _device_for_backend()
-    shapes = [None] * n_partitions
-    for p, a in local.items():
-        shapes[p] = a.shape
-    # every rank learns every shape (tiny object collective)
-    all_shapes = [None] * ws
-    dist.all_gather_object(all_shapes, {p: a.shape for p, a in local.items()})
-    for d in all_shapes:
-        for p, sh in d.items():
-            shapes[p] = tuple(sh)
-    rmax = max(s[0] for s in shapes)
-    cmax = max(s[1] for s in shapes)
-    slots = (n_partitions + ws - 1) // ws
+    dev = _device_for_backend()      # before the object collective: it sends on the current device
+    held = [None] * ws
+    dist.all_gather_object(held, {int(p): tuple(a.shape) for p, a in local.items()})
+    where, shapes = {}, {}
+    for r, dct in enumerate(held):
+        for k, p in enumerate(sorted(dct)):
+            where[p] = (r, k)
+            shapes[p] = tuple(dct[p])
+    missing = [p for p in range(n_partitions) if p not in where]
+    if missing:
+        raise ValueError(f"partitions {missing} are held by no rank")
+    rmax = max(sh[0] for sh in shapes.values())
+    cmax = max(sh[1] for sh in shapes.values())
+    slots = max(1, max(len(dct) for dct in held))
     buf = torch.zeros((slots, rmax, cmax), dtype=torch.float64, device=dev)
-    for k, p in enumerate(local_partitions(n_partitions, rank, ws)):
+    for k, p in enumerate(sorted(local)):
         a = torch.as_tensor(np.ascontiguousarray(local[p]), dtype=torch.float64)
         buf[k, : a.shape[0], : a.shape[1]] = a.to(dev)
     out = [torch.empty_like(buf) for _ in range(ws)]
     dist.all_gather(out, buf)
     res = []
     for p in range(n_partitions):
-        r, k = p % ws, p // ws
+        r, k = where[p]
         rr, cc = shapes[p]
         res.append(out[r][k, :rr, :cc].cpu().numpy().copy())
     return res

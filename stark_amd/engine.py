@@ -414,9 +414,15 @@ def consensus(draws, ctx: Context | None = None, separate_lp: bool = False):
     ctx = ctx or default_context()
     if separate_lp:
         d = [np.asarray(x, np.float64) for x in draws]
-        th, used_t = consensus([x[:-1] for x in d], ctx)
-        lp, _ = consensus([x[-1:] for x in d], ctx)
-        return np.vstack([th, lp]), used_t
+        # one NaN mask over the whole rows, so both blocks combine the same shard set
+        keep = [i for i, x in enumerate(d) if not np.isnan(x).any()]
+        used = np.zeros(len(d), bool)
+        used[keep] = True
+        if not keep:
+            consensus(d, ctx)               # raises the library's "every shard holds NaN draws"
+        th, _ = consensus([d[i][:-1] for i in keep], ctx)
+        lp, _ = consensus([d[i][-1:] for i in keep], ctx)
+        return np.vstack([th, lp]), used
     X, (P, S) = _stack(draws)
     out = np.empty((P, S))
     used = np.empty(len(draws), np.int32)

@@ -147,7 +147,11 @@ def pack_data(family: str, data: dict) -> dict:
         y = np.asarray(data["y"]).reshape(-1)
         if y.shape[0] != N:
             raise ValueError("y must have N entries")
-        return {"x": x, "y": y.astype(np.int32)}
+        # int<lower=0, upper=1> y[N]: pystan rejects non-integer or out-of-range values
+        yf = y.astype(np.float64)
+        if not np.all(yf == np.round(yf)) or np.any((yf != 0) & (yf != 1)):
+            raise ValueError("bernoulli_logit data: y must hold the integers 0 and 1")
+        return {"x": x, "y": yf.astype(np.int32)}
     y = np.asarray(data["y"], np.float64).reshape(-1)
     if y.shape[0] != N:
         raise ValueError("y must have N entries")

@@ -18,8 +18,10 @@ Deliberate deviations from the reference code, each mirroring its evident intent
 (DESIGN.md "Reference bugs"): the combine accepts any number of partitions (the reference
 reducer only works for two); shards with NaN draws are left out of the combine; naive
 mode runs ``n`` full-data replicas (the reference's non-accumulating ``union`` runs the
-partitions plus one full copy -- available as ``distribute(..., reference_union=True)``);
-draws are returned in chain order (pystan's ``extract(permuted=True)`` shuffles them).
+partitions plus one full copy -- available as ``distribute(..., reference_union=True)``).
+Draws follow pystan's ``fit.extract()`` (``permuted=True``, stark/stark.py:49): each chain's
+post-warmup draws in a seeded random order, chains concatenated; ``permuted=False`` keeps
+chain order (what the sampler's diagnostics need).
 """
 from __future__ import annotations
 
@@ -40,9 +42,10 @@ def consensus_avg(J):
     def c(f1, f2):
         if isinstance(f1, list):
             sw, swt = f1
-            w2, w2t, used = engine.consensus_products([np.asarray(f2, np.float64)])
-            if not used[0]:
+            f2 = np.asarray(f2, np.float64)
+            if np.isnan(f2).any():          # a NaN shard later in the reduce is left out
                 return [sw, swt]
+            w2, w2t, _ = engine.consensus_products([f2])
             return [sw + w2, swt + w2t]
         f1 = np.asarray(f1, np.float64)
         if np.isnan(f1).any():
@@ -56,6 +59,27 @@ def consensus_avg(J):
 def concatenate_samples(a, b):
     """stark/stark.py:23-24."""
     return np.vstack((a, b))
+
+
+def permute_draws(draws, chains: int, seed: int, partition: int):
+    """pystan 2 ``extract(permuted=True)`` order for one partition's P x (chains * n) matrix
+    (chain-major columns): every chain's n draws in a random order, chains concatenated.
+    The permutation is a pure function of (seed, partition, chain) -- numpy's Philox
+    counter-based generator keyed by the sampling seed -- so a run is reproducible on 1 or N
+    GPUs.  (pystan draws its permutations from numpy's global RandomState; the order is
+    arbitrary either way, what matters to the reference's combine is that draw i of every
+    partition is paired after the shuffle, stark/stark.py:20.)"""
+    draws = np.asarray(draws)
+    P, S = draws.shape
+    if S % chains:
+        raise ValueError("draw columns must be chains x draws")
+    n = S // chains
+    cols = []
+    for c in range(chains):
+        g = np.random.Generator(np.random.Philox(key=[int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                                      (int(partition) << 32) | int(c)]))
+        cols.append(c * n + g.permutation(n))
+    return np.ascontiguousarray(draws[:, np.concatenate(cols)]) if cols else draws
 
 
 def _extract_to_matrix(extract):
@@ -156,9 +180,10 @@ class Stark:
         self.stan_kwargs = kwargs
 
     # ---- per-partition sampling (stark/stark.py:41-57), batched over partitions
-    def _sample_partitions(self, datas, shard_ids=None, **kwargs):
+    def _sample_partitions(self, datas, shard_ids=None, permuted=True, **kwargs):
         """Run every data dict as one shard of a single GPU model; returns one P x S matrix
-        per data dict, rows in extract() order (params, transformed params, lp__).
+        per data dict, rows in extract() order (params, transformed params, lp__), columns in
+        ``extract(permuted=True)`` order (``permute_draws``) unless permuted=False.
         shard_ids: global partition index of each data dict (keys the RNG streams, so a
         partition samples identically on 1 or N GPUs)."""
         if self.family is None:
@@ -175,7 +200,10 @@ class Stark:
         finally:
             model.close()
         self.last_run = res
-        return res.draws
+        if not permuted:
+            return res.draws
+        ids = shard_ids if shard_ids is not None else range(len(datas))
+        return [permute_draws(d, cfg["chains"], cfg["seed"], p) for d, p in zip(res.draws, ids)]
 
     def _mcmc(self, callback, **kwargs):
         def w(sts):
@@ -202,9 +230,14 @@ class Stark:
 
     def concensusWeight(self, separate_lp=False, **kwargs):
         """stark/stark.py:59-71: subposterior per partition, consensus weighted average.
-        The default combines every extract() row jointly, lp__ included, as the reference does;
-        separate_lp=True gives lp__ its own weight block so the parameter rows are combined
-        from the parameters' covariance alone (engine.consensus)."""
+
+        The default reproduces the REFERENCE's combine, for parity: every extract() row is
+        combined jointly, lp__ included.  That is not the accurate choice: each shard's lp__
+        sits at its own offset, many lp__ sds from the others, and the sampled lp__-parameter
+        cross-covariances turn that offset into an error of the parameter means (mean z^2 of
+        4-7 at N = 1e8).  For accuracy pass separate_lp=True: lp__ gets a
+        1 x 1 weight block of its own and the parameters are combined from their own
+        covariance (engine.consensus).  permuted=False keeps chain order in the draws."""
         kwargs = self._defaults(kwargs)
         parts = _rdd.partitions_of(self.rdd)
         subposteriors = self._run_distributed(parts, **kwargs)

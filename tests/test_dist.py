@@ -124,3 +124,87 @@ def test_gloo_world2_fulldata_exchange():
         assert p.exitcode == 0
     assert all(r[1] for r in res)
     assert res[0][2] == (0, 500) and res[1][2] == (500, 501)
+
+
+# ---------------------------------------------------------------- bench exchange (ESS / accuracy phase)
+def _bench_exchange_worker(rank, world, port, q):
+    """bench.py's N-rank tail on gloo: each rank holds 2 of 4 logistic shards (oracle models
+    stand in for the GPU gradient), the draw matrices are all-gathered in partition order, and
+    the full-data Laplace reference is formed from per-rank gradient sums all-reduced over the
+    group -- every rank must take the same Newton steps and end at the single-process MAP."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from stark_amd import dist as sdist
+        from tools import laplace as L
+        O.build()
+        n, d, S = 3000, 5, 4
+        X = O.gen_x(9, 0, n * S, d)
+        beta = O.gen_beta(9, d)
+        y, _ = O.gen_y_logistic(9, 0, X, 0.2, beta)
+        mine = list(range(rank * S // world, (rank + 1) * S // world))
+
+        class Shards:
+            def __init__(self, ids):
+                self.m = [O.Model(O.FAM_LOGREG, X=X[k * n:(k + 1) * n], y=y[k * n:(k + 1) * n]) for k in ids]
+
+            def log_density_grad(self, s, Q):
+                out = [self.m[s].lpgrad(qq) for qq in np.atleast_2d(Q)]
+                return np.array([o[0] for o in out]), np.array([o[1] for o in out])
+
+        def allreduce(arr):
+            t = torch.from_numpy(np.ascontiguousarray(arr))
+            dist.all_reduce(t)
+            arr[...] = t.numpy()
+
+        local = {k: np.full((3, 8), float(k)) + rank * 0 for k in mine}
+        allp = sdist.all_gather_partitions(local, S)
+        gathered_ok = all(np.array_equal(allp[k], np.full((3, 8), float(k))) for k in range(S))
+        q0 = np.zeros(d + 1)
+        sd0 = np.full(d + 1, 0.02)
+        m_, c_, info = L.laplace(Shards(mine), list(range(len(mine))), q0, sd0, reduce=allreduce)
+        q.put((rank, gathered_ok, m_, c_, info["newton_steps_in_sd"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_exchange():
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    from tools import laplace as L
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] and res[1][1]
+    np.testing.assert_array_equal(res[0][2], res[1][2])           # identical Newton paths on both ranks
+    assert res[0][4] == res[1][4]
+    # single process, all 4 shards: the same MAP (sums differ only in association order)
+    O.build()
+    n, d, S = 3000, 5, 4
+    X = O.gen_x(9, 0, n * S, d)
+    beta = O.gen_beta(9, d)
+    y, _ = O.gen_y_logistic(9, 0, X, 0.2, beta)
+    full = O.Model(O.FAM_LOGREG, X=X, y=y)
+
+    class One:
+        def log_density_grad(self, s, Q):
+            out = [full.lpgrad(qq) for qq in np.atleast_2d(Q)]
+            return np.array([o[0] for o in out]), np.array([o[1] for o in out])
+
+    m1, c1, _ = L.laplace(One(), [0], np.zeros(d + 1), np.full(d + 1, 0.02))
+    sd = np.sqrt(np.diag(c1))
+    assert np.abs((res[0][2] - m1) / sd).max() < 1e-6
+    np.testing.assert_allclose(res[0][3], c1, rtol=1e-5)

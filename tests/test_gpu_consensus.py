@@ -1,0 +1,189 @@
+"""Consensus combine of SAMPLED subposteriors against the full-data posterior -- the
+north_star's "matching the posterior moments within MCSE" (BASELINE.json) and the result
+contract of the reference's own test (test/stark_test.py:25-50).
+
+The consensus estimator's Monte Carlo error includes the noise of its sampled weights
+W_s = inv(cov(draws_s)) (stark/stark.py:17), which the ESS of the combined draws does not
+see.  Its MCSE is therefore measured by batches: every shard's chains are split into G
+groups, each group set is combined on its own, and the spread of the G consensus means,
+pooled over parameters (relative to the posterior sd), gives the standard error of the
+full-run estimator.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from stark_amd.diagnostics import ess
+
+pytestmark = pytest.mark.gpu
+
+
+def _chain_major(dr, chains, n):
+    return np.ascontiguousarray(dr[:, :chains * n])
+
+
+def _batch_mcse_rel(draws, chains, n, ctx, sd, groups=4):
+    """Pooled relative MCSE of the consensus means of the first len(sd) rows (sampled
+    weights included; lp__ combined in its own block)."""
+    from stark_amd import engine
+    cg = chains // groups
+    k = len(sd)
+    gm = []
+    for g in range(groups):
+        sel = [np.ascontiguousarray(d[:, g * cg * n:(g + 1) * cg * n]) for d in draws]
+        c, _ = engine.consensus(sel, ctx, separate_lp=True)
+        gm.append(c[:k].mean(1))
+    var = np.var(np.array(gm), axis=0, ddof=1) / groups
+    return float(np.sqrt(np.mean(var / sd ** 2)))
+
+
+def test_linear_8_shards_consensus_matches_closed_form(ctx, orc):
+    """BASELINE configs[2] shape (d = 50, 8 subposterior shards), at 8 x 5000 rows: the
+    consensus of the sampled shards vs the exact full-data posterior of (alpha, beta) (flat
+    priors: multivariate t, oracle.linreg_exact_moments) -- means within the consensus
+    estimator's MCSE, sds within 6 %."""
+    from stark_amd import engine
+    d, S, n_s, C, nw, ns = 50, 8, 5000, 16, 300, 300
+    X = orc.gen_x(41, 0, S * n_s, d)
+    beta = orc.gen_beta(41, d)
+    y = orc.gen_y_linear(41, 0, X, 0.3, beta)
+    shards = [{"x": X[k * n_s:(k + 1) * n_s], "y": y[k * n_s:(k + 1) * n_s]} for k in range(S)]
+    m = engine.Model(ctx, "linear", shards)
+    res = m.sample(num_warmup=nw, num_samples=ns, chains=C, seed=7)
+    info = res.info
+    assert info["errors"] == 0
+    assert info["divergent"] == 0, info
+    draws = [_chain_major(x, C, ns) for x in res.draws]            # P = 53: alpha, beta[50], sigma, lp__
+    comb, used = engine.consensus(draws, ctx, separate_lp=True)
+    assert used.all()
+    mean, cov = orc.linreg_exact_moments(X, y)
+    sd = np.sqrt(np.diag(cov))
+    k = d + 1
+    cm, csd = comb[:k].mean(1), comb[:k].std(1)
+    rel = _batch_mcse_rel(draws, C, ns, ctx, sd)
+    z = (cm - mean) / (rel * sd)
+    assert np.mean(z ** 2) < 2.5, (np.mean(z ** 2), rel)
+    assert np.abs(z).max() < 4.5, (np.abs(z).max(), rel)
+    assert np.all(np.abs(csd / sd - 1) < 0.06), (csd / sd).min()
+    # per-shard sanity: every subposterior is centred on its own OLS fit
+    for s in range(S):
+        ms, cs = orc.linreg_exact_moments(shards[s]["x"], shards[s]["y"])
+        zs = (draws[s][:k].mean(1) - ms) / np.sqrt(np.diag(cs))
+        assert np.mean(zs ** 2) < 0.05, (s, np.mean(zs ** 2))
+    m.close()
+
+
+def test_logistic_8_shards_consensus_matches_fulldata_sampler(ctx):
+    """Logistic regression d = 100 (BASELINE configs[3] shape) at 8 x 2e5 rows: the
+    consensus of 8 sampled subposteriors vs the full-data posterior of the same 1.6e6 rows,
+    sampled by the same GPU NUTS as one shard, and vs its Laplace approximation (MAP and
+    inverse Hessian from the GPU gradient, tools/laplace.py)."""
+    from stark_amd import engine
+    from tools import laplace as L
+    d, S, n_s, C, nw, ns = 100, 8, 200_000, 16, 200, 250
+    m = engine.Model.synthetic(ctx, "logistic", S, n_s, d, data_seed=77)
+    res = m.sample(num_warmup=nw, num_samples=ns, chains=C, seed=3, stepsize_jitter=0.5)
+    assert res.info["errors"] == 0
+    draws = [_chain_major(x, C, ns) for x in res.draws]
+    comb, _ = engine.consensus(draws, ctx, separate_lp=True)
+    full = engine.Model.synthetic(ctx, "logistic", 1, S * n_s, d, data_seed=77)
+    fres = full.sample(num_warmup=nw, num_samples=ns, chains=C, seed=4, stepsize_jitter=0.5)
+    fd = fres.draws[0][:-1]
+    fm, fsd = fd.mean(1), fd.std(1)
+    f_mcse = np.array([fsd[p] / np.sqrt(ess(fd[p].reshape(C, ns))) for p in range(d + 1)])
+    rel = _batch_mcse_rel(draws, C, ns, ctx, fsd)
+    se = np.sqrt((rel * fsd) ** 2 + f_mcse ** 2)
+    cm, csd = comb[:-1].mean(1), comb[:-1].std(1)
+    z = (cm - fm) / se
+    assert np.mean(z ** 2) < 2.5, (np.mean(z ** 2), rel)
+    assert np.all(np.abs(csd / fsd - 1) < 0.12), ((csd / fsd).min(), (csd / fsd).max())
+    # the same against the full-data Laplace reference (Gaussian to ~d/sqrt(N) sd here)
+    pooled = np.hstack([x[:-1] for x in draws])
+    lm, lc, _ = L.laplace(full, [0], fm, fsd)
+    lsd = np.sqrt(np.diag(lc))
+    assert np.all(np.abs(fsd / lsd - 1) < 0.1)
+    zl = (cm - lm) / lsd
+    assert np.sqrt(np.mean(zl ** 2)) < 0.25, np.sqrt(np.mean(zl ** 2))
+    assert pooled.shape[0] == d + 1
+    m.close()
+    full.close()
+
+
+def test_reference_contract_schools(ctx, orc):
+    """test/stark_test.py:25-50 as the reference intends it: 8 schools in 2 partitions,
+    distribute(n=4) draws' means within L2 1.5 of the posterior means over the 19 extract()
+    rows (here exact, by quadrature, instead of a 4-chain pystan run), and a weighted run of
+    P x S draws (stark/stark.py:56; the stale test's (1000, 19) is neither the code's layout
+    nor its partition size).  The weighted mu -- the one row whose meaning both 4-school
+    partitions share -- lies within 2 sd of the full-data mean."""
+    from stark_amd import stark
+    from stark_amd.rdd import LocalContext
+    sc = LocalContext()
+    school = list(zip([28, 8, -3, 7, -1, 1, 18, 12], [15, 10, 16, 11, 9, 11, 10, 18]))
+
+    def prep(data):
+        return {"J": len(data), "y": [d[0] for d in data], "sigma": [d[1] for d in data]}
+
+    st = stark.Stark(sc, sc.parallelize(school, 2), prep)
+    st.setStanModel(file=os.path.join(os.path.dirname(os.path.dirname(__file__)), "stark_amd", "models",
+                                      "schools.stan"))
+    target = orc.schools_exact_extract_means(orc.SCHOOLS_Y, orc.SCHOOLS_SIGMA)
+    sp_fit = st.distribute(n=4, seed=11)
+    assert sp_fit.shape == (4 * 19, 1000)
+    means = sp_fit.reshape(4, 19, 1000).mean(axis=(0, 2))
+    assert np.linalg.norm(target - means) < 1.5, np.linalg.norm(target - means)
+    sp_wa = st.concensusWeight(seed=12, separate_lp=True)
+    assert sp_wa.shape == (11, 1000) and np.isfinite(sp_wa).all()
+    assert abs(sp_wa[0].mean() - target[0]) < 2 * 5.3, sp_wa[0].mean()    # posterior sd of mu ~ 5.3
+
+
+def test_stark_over_single_rank_rccl_group(ctx):
+    """The Stark driver inside an initialised RCCL group (world size 1): partitions placed by
+    rank, the P x S matrices exchanged by the real collective (all_gather_object + a device
+    all_gather on cuda:LOCAL_RANK), result equal to the run without a process group."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from stark_amd import stark
+    from stark_amd.rdd import LocalContext
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    sc = LocalContext()
+    school = list(zip([28, 8, -3, 7, -1, 1, 18, 12], [15, 10, 16, 11, 9, 11, 10, 18]))
+
+    def prep(data):
+        return {"J": len(data), "y": [d[0] for d in data], "sigma": [d[1] for d in data]}
+
+    path = os.path.join(os.path.dirname(os.path.dirname(__file__)), "stark_amd", "models", "schools.stan")
+    st = stark.Stark(sc, sc.parallelize(school, 2), prep)
+    st.setStanModel(file=path)
+    ref = st.concensusWeight(iter=400, seed=5)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK="0")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        got = st.concensusWeight(iter=400, seed=5)
+        assert torch.cuda.current_device() == 0
+    finally:
+        dist.destroy_process_group()
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_consensus_avg_reduce_skips_nan_in_any_position(ctx, orc):
+    """functools.reduce of the GPU reducer over 3 shards with NaN draws in the LAST one:
+    the NaN shard is left out (the evident intent of stark/stark.py:9-10), not a crash."""
+    import functools
+    from stark_amd import engine, stark
+    rng = np.random.default_rng(5)
+    f = [rng.normal(size=(6, 400)) + np.arange(6)[:, None] for _ in range(3)]
+    bad = f[2].copy()
+    bad[3, 17] = np.nan
+    sw, swt = functools.reduce(stark.consensus_avg(3), [f[0], f[1], bad])
+    out = engine.consensus_solve(sw, swt, ctx)
+    ref = orc.consensus_combine_ref([f[0], f[1]])
+    np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-11)
+    sep, used = engine.consensus([f[0], f[1], bad], ctx, separate_lp=True)
+    assert list(used) == [True, True, False]
+    np.testing.assert_allclose(sep[:-1], orc.consensus_combine_ref([x[:-1] for x in f[:2]]), rtol=1e-9, atol=1e-11)

@@ -202,3 +202,60 @@ def test_recognise_priors():
     with pytest.raises(NotImplementedError):
         frontend.program_info(sch)
     assert frontend.load_program_info(family="logistic", priors={"beta": 2.0}) == ("logistic", {"beta": 2.0})
+
+
+def test_permute_draws_is_pystan_extract_order():
+    """extract(permuted=True) (stark/stark.py:49): each chain's draws shuffled, chains
+    concatenated; a pure function of (seed, partition, chain)."""
+    from stark_amd.stark import permute_draws
+    chains, n = 3, 50
+    d = np.vstack([np.arange(chains * n, dtype=np.float64), -np.arange(chains * n, dtype=np.float64)])
+    p = permute_draws(d, chains, seed=7, partition=2)
+    for c in range(chains):
+        blk = p[0, c * n:(c + 1) * n]
+        assert sorted(blk) == list(range(c * n, (c + 1) * n))     # chain c's draws stay in block c
+        assert not np.array_equal(blk, np.arange(c * n, (c + 1) * n))
+    np.testing.assert_array_equal(p[1], -p[0])                    # columns move whole (every row)
+    np.testing.assert_array_equal(p, permute_draws(d, chains, seed=7, partition=2))
+    assert not np.array_equal(p, permute_draws(d, chains, seed=7, partition=3))
+    with pytest.raises(ValueError):
+        permute_draws(d[:, :-1], chains, seed=1, partition=0)
+
+
+def test_logistic_y_must_be_binary_integers():
+    from stark_amd import frontend
+    ok = frontend.pack_data("logistic", {"N": 3, "K": 1, "x": [[1.0], [2.0], [3.0]], "y": [0.0, 1.0, 1]})
+    assert ok["y"].tolist() == [0, 1, 1]
+    for bad in ([0, 0.5, 1], [0, 1.9, 1], [0, 2, 1], [-1, 0, 1]):
+        with pytest.raises(ValueError):
+            frontend.pack_data("logistic", {"N": 3, "K": 1, "x": [[1.0], [2.0], [3.0]], "y": bad})
+
+
+def test_ess_stan219_has_no_floor():
+    """Stan 2.19's estimator has no tau_hat floor; the later releases' one is opt-in."""
+    from stark_amd.diagnostics import ess
+    x = np.tile([1.0, -1.0], 500)[None, :] + 1e-9 * np.arange(1000)[None, :]   # antithetic
+    assert ess(x) > ess(x, floor=True)
+    assert ess(x, floor=True) <= 1000 * np.log10(1000) + 1e-6
+
+
+def test_laplace_reference_matches_closed_form_gaussian():
+    """tools/laplace.py on a model with an exactly quadratic log density: MAP and covariance
+    exact (the Newton step and the difference Hessian are exact for a quadratic)."""
+    from tools import laplace as L
+    rng = np.random.default_rng(3)
+    D = 7
+    A = rng.normal(size=(D, D))
+    prec = A @ A.T + D * np.eye(D)
+    mu = rng.normal(size=D)
+
+    class Quad:
+        def log_density_grad(self, s, Q):
+            Q = np.atleast_2d(Q)
+            r = Q - mu
+            part = prec / 2.0                       # two "shards" of half the precision each
+            return -0.5 * np.einsum("ij,jk,ik->i", r, part, r), -(r @ part)
+
+    m, c, info = L.laplace(Quad(), [0, 1], mu + 0.3, np.ones(D))
+    np.testing.assert_allclose(m, mu, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(c, np.linalg.inv(prec), rtol=1e-7, atol=1e-10)
