@@ -234,9 +234,13 @@ def test_logistic_y_must_be_binary_integers():
 def test_ess_stan219_has_no_floor():
     """Stan 2.19's estimator has no tau_hat floor; the later releases' one is opt-in."""
     from stark_amd.diagnostics import ess
-    x = np.tile([1.0, -1.0], 500)[None, :] + 1e-9 * np.arange(1000)[None, :]   # antithetic
+    rng = np.random.default_rng(1)
+    x = np.zeros(4000)
+    e = rng.normal(size=4000)
+    for t in range(1, 4000):
+        x[t] = -0.9 * x[t - 1] + e[t]                     # antithetic AR(1): tau = 1/19
     assert ess(x) > ess(x, floor=True)
-    assert ess(x, floor=True) <= 1000 * np.log10(1000) + 1e-6
+    assert abs(ess(x, floor=True) - 4000 * np.log10(4000)) < 1e-6 * 4000
 
 
 def test_laplace_reference_matches_closed_form_gaussian():
