@@ -348,11 +348,14 @@ def main():
     total_grads = info["grad_evals"] * world
     cpu = None
     if not a.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(a.d, rows_per_shard, a.shards, a.cpu_baseline_seconds, a.family)
-        cpu["ess_per_sec"] = cpu["value"] * ess_c / total_grads
-        cpu["ess_note"] = ("the measured CPU gradient rate x this run's ESS per gradient evaluation "
-                           "(warmup included): the CPU twin runs the same NUTS transitions")
-        cpu.update(cpu_combine(allp))
+        try:
+            cpu = cpu_baseline(a.d, rows_per_shard, a.shards, a.cpu_baseline_seconds, a.family)
+            cpu["ess_per_sec"] = cpu["value"] * ess_c / total_grads
+            cpu["ess_note"] = ("the measured CPU gradient rate x this run's ESS per gradient evaluation "
+                               "(warmup included): the CPU twin runs the same NUTS transitions")
+            cpu.update(cpu_combine(allp))
+        except Exception as e:          # the GPU line is still printed
+            cpu = {"error": repr(e)}
     line = {
         "metric": f"gradient evals/sec (whole node), {a.family} regression N={a.rows:.0e} d={a.d}".replace("e+0", "e"),
         "value": value,

@@ -229,7 +229,7 @@ def consensus_combine_ref(draws):
     for f in draws:
         if np.isnan(f).any():
             continue
-        w = np.linalg.inv(np.cov(f))
+        w = np.linalg.inv(np.atleast_2d(np.cov(f)))       # a 1-row block (lp__ alone): 1 x 1
         sw = w if sw is None else sw + w
         wt = np.dot(w, f)
         swt = wt if swt is None else swt + wt

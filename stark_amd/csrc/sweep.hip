@@ -18,6 +18,7 @@
 #include "common.h"
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
 #include <algorithm>
 #include <set>
 #include <type_traits>
@@ -1178,6 +1179,241 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   }
 }
 
+// v4r: the v4 sub-tile computation with the NEXT sub-tile streamed through registers.
+//
+// In k_sweepe the next sub-tile's DMA is issued after the forward and must land before the
+// next forward, i.e. within the residual + backward of one sub-tile (plus what the SIMD's
+// other wave does meanwhile); under full-chip streaming the HBM latency is longer than that
+// and the waves wait at vmcnt(0) (PMC: MFMA busy 56 %, f64 VALU 15 %, ~29 % idle).  Here each
+// wave keeps PF sub-tiles in flight in VGPRs (global -> VGPR buffer loads, 16 B per lane per
+// instruction, 1 KiB contiguous per wave-instruction): sub-tile k+1's loads are issued right
+// after sub-tile k has been written into the slot, so they have a whole iteration (PF = 1) or
+// two (PF = 2) to land; at the end of the iteration the wave writes them into its LDS slot
+// (ds_write_b128, conflict-free: piece p at byte 16 p) and issues the next loads.  The slot
+// is never shared, so the backward reads its A operands straight from the slot (no register
+// copy) and the slot costs the same LDS as k_sweepe.  Arithmetic, operand layouts, sums and
+// their order are exactly k_sweepe's, so the results are bitwise identical.
+typedef unsigned int stk_u4 __attribute__((ext_vector_type(4)));
+template <int NP>
+struct SubtileRegs {                 // one 16-row sub-tile: NP 16-B pieces per lane + y
+  stk_u4 x[NP];
+  uint64_t y;
+};
+template <int FAM, int KF, int JT, int PF = 1>
+__global__ __launch_bounds__(256, 2) void k_sweepr(SweepArgs A) {
+  constexpr int C = SM_C, NW = SM_W, JTV = JT - 1, KP = 4 * KF;
+  constexpr int D = KP;                               // d = 4 KF for the shapes this serves
+  constexpr int SBX = SM_R * D * 8;                   // X bytes of a sub-tile
+  constexpr int NPC = SBX / 16;                       // 16-B pieces of a sub-tile
+  constexpr int NP = (NPC + 63) / 64;                 // pieces per lane
+  constexpr int LASTL = NPC - 64 * (NP - 1);          // lanes holding a piece in the last round
+  constexpr int YB = (FAM == STK_LOGREG) ? 4 : 8;
+  static_assert(SBX % 16 == 0 && LASTL > 0 && PF >= 1 && PF <= 2, "k_sweepr geometry");
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + 63) / 64;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * 64, r1 = std::min<int64_t>(sh.n, t1 * 64);
+  const int nrows = (int)(r1 - r0);
+  const int nsub = (nrows + SM_R - 1) / SM_R;
+  const int mine = nsub > w ? (nsub - w + NW - 1) / NW : 0;
+  constexpr int SS = SBX + 128;
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const slot = reinterpret_cast<char*>(lds) + (size_t)w * SS;
+  double* const bimg = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);  // [16][KP]
+  double* const sptab = bimg + C * KP;
+  if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
+  const double* qs = A.q + (size_t)shard * C * A.Dp;
+  for (int i = tid; i < C * KP; i += NW * 64) {
+    const int c = i / KP, col = i % KP;
+    bimg[i] = qs[(size_t)c * A.Dp + 1 + col];
+  }
+  const double alpha = qs[(size_t)lr * A.Dp];
+  const double inv_s = (FAM == STK_LINREG) ? exp(-qs[(size_t)lr * A.Dp + D + 1]) : 0.0;
+  __syncthreads();
+
+  // rows past the chunk read as zeros (buffer range check) and are masked in the residual
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * D, (int64_t)nrows * D * 8);
+  const void* ybase = (FAM == STK_LOGREG) ? (const void*)(sh.yi + r0) : (const void*)(sh.y + r0);
+  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(ybase, (int64_t)nrows * YB);
+  auto load = [&](SubtileRegs<NP>& b, int k) {
+    const int xoff = (w + NW * k) * SBX;
+#pragma unroll
+    for (int j = 0; j < NP - 1; ++j) b.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, lane * 16 + j * 1024, xoff, 0);
+    b.x[NP - 1] = lane < LASTL ? __builtin_amdgcn_raw_buffer_load_b128(xr, lane * 16 + (NP - 1) * 1024, xoff, 0)
+                               : stk_u4{0u, 0u, 0u, 0u};
+    const int yoff = (w + NW * k) * SM_R * YB;
+    if constexpr (YB == 4) {
+      b.y = lane < SM_R ? (uint64_t)__builtin_amdgcn_raw_buffer_load_b32(yr, lane * 4, yoff, 0) : 0u;
+    } else {
+      b.y = 0;
+      if (lane < SM_R) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(yr, lane * 8, yoff, 0);
+        b.y = __builtin_bit_cast(uint64_t, v);
+      }
+    }
+  };
+  auto store = [&](const SubtileRegs<NP>& b) {
+#pragma unroll
+    for (int j = 0; j < NP - 1; ++j) *reinterpret_cast<stk_u4*>(slot + lane * 16 + j * 1024) = b.x[j];
+    if (lane < LASTL) *reinterpret_cast<stk_u4*>(slot + lane * 16 + (NP - 1) * 1024) = b.x[NP - 1];
+    if (lane < SM_R) {
+      if constexpr (YB == 4) *reinterpret_cast<uint32_t*>(slot + SBX + lane * 4) = (uint32_t)b.y;
+      else *reinterpret_cast<uint64_t*>(slot + SBX + lane * 8) = b.y;
+    }
+  };
+
+  dbl4 gacc[JTV];
+#pragma unroll
+  for (int t = 0; t < JTV; ++t) gacc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double gv[4] = {0.0, 0.0, 0.0, 0.0};
+  double lpa = 0.0, gaa = 0.0;
+  const double* xs = reinterpret_cast<const double*>(slot);
+  const double* brow = bimg + lr * KP + lh * KF;
+
+  auto compute = [&](int k) {
+    const int rv = std::min(SM_R, nrows - SM_R * (w + NW * k));
+    // ---- forward
+    dbl4 ea[SE_NACC];
+#pragma unroll
+    for (int i = 0; i < SE_NACC; ++i) ea[i] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const double* xrow = xs + lr * D;
+#pragma unroll
+    for (int s = 0; s < KF; ++s) ea[s % SE_NACC] = mfma_f64(xrow[lh * KF + s], brow[s], ea[s % SE_NACC]);
+    dbl4 e0 = ea[0], e1 = ea[1];
+#pragma unroll
+    for (int i = 2; i < SE_NACC; ++i) { if (i & 1) e1 += ea[i]; else e0 += ea[i]; }
+    const dbl4 eta4 = e0 + e1;
+    // ---- residual
+    double de[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool valid = lh + 4 * i < rv;
+      const double eta = eta4[i] + alpha;
+      double dv, lt;
+      if constexpr (FAM == STK_LOGREG) {
+        const double yv = (double)*reinterpret_cast<const int32_t*>(slot + SBX + (lh + 4 * i) * 4);
+        const double sgn = 2.0 * yv - 1.0;
+        const double ntt = sgn * eta;
+        double e, lm, wt;
+        softplus_tab(ntt, sptab, &e, &lm, &wt);
+        const bool hi = ntt > 20.0, lo = ntt < -20.0;
+        lt = hi ? -e : (lo ? ntt : -lm);
+        dv = sgn * (hi ? e : (lo ? 1.0 : wt));
+      } else {
+        const double yv = *reinterpret_cast<const double*>(slot + SBX + (lh + 4 * i) * 8);
+        const double z = (yv - eta) * inv_s;
+        lt = z * z;
+        dv = z * inv_s;
+      }
+      dv = valid ? dv : 0.0;
+      lpa += valid ? lt : 0.0;
+      gaa += dv;
+      de[i] = dv;
+    }
+    // ---- backward (A operands straight from the slot)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < JTV; ++t) gacc[t] = mfma_f64(xs[(lh + 4 * s) * D + 16 * t + lr], de[s], gacc[t]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const dbl2* p = reinterpret_cast<const dbl2*>(xs + (lh + 4 * i) * D + 16 * JTV);
+      const dbl2 a0 = p[0], a1 = p[1];
+      gv[0] = fma(a0.x, de[i], gv[0]);
+      gv[1] = fma(a0.y, de[i], gv[1]);
+      gv[2] = fma(a1.x, de[i], gv[2]);
+      gv[3] = fma(a1.y, de[i], gv[3]);
+    }
+  };
+
+  if constexpr (PF == 1) {
+    SubtileRegs<NP> b;
+    if (mine > 0) {
+      load(b, 0);
+      store(b);
+    }
+    if (mine > 1) load(b, 1);
+    for (int k = 0; k < mine; ++k) {
+      compute(k);
+      if (k + 1 < mine) {
+        __builtin_amdgcn_sched_barrier(0);
+        store(b);                                      // waits for sub-tile k+1's loads
+        if (k + 2 < mine) load(b, k + 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else {
+    // two sub-tiles in flight: b0 holds the even ones, b1 the odd ones
+    SubtileRegs<NP> b0, b1;
+    if (mine > 0) {
+      load(b0, 0);
+      store(b0);
+    }
+    if (mine > 1) load(b1, 1);
+    if (mine > 2) load(b0, 2);
+    for (int k = 0; k < mine; k += 2) {
+      compute(k);
+      if (k + 1 < mine) {
+        __builtin_amdgcn_sched_barrier(0);
+        store(b1);
+        if (k + 3 < mine) load(b1, k + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(k + 1);
+        if (k + 2 < mine) {
+          __builtin_amdgcn_sched_barrier(0);
+          store(b0);
+          if (k + 4 < mine) load(b0, k + 4);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  }
+
+  // ---- fixed-order block reduction (as k_sweepe)
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __syncthreads();
+  double* red = lds;
+  constexpr int JC = JT * 16;
+#pragma unroll
+  for (int t = 0; t < JTV; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[((size_t)w * JC + 16 * t + lh + 4 * i) * 16 + lr] = gacc[t][i];
+  double* red2 = red + (size_t)NW * JC * 16;
+  red2[(size_t)tid * 2 + 0] = lpa;
+  red2[(size_t)tid * 2 + 1] = gaa;
+  double* red3 = red2 + (size_t)NW * 64 * 2;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) red3[((size_t)(w * 4 + lh) * 4 + jj) * 16 + lr] = gv[jj];
+  __syncthreads();
+  double* out = A.partial + ((size_t)shard * A.Gs + chunk) * C * A.PW;
+  constexpr int jv = 16 * JTV;
+  for (int i = tid; i < C * D; i += NW * 64) {
+    const int c = i / D, j = i % D;
+    double v = 0.0;
+    if (j < jv) {
+      for (int ww = 0; ww < NW; ++ww) v += red[((size_t)ww * JC + j) * 16 + c];
+    } else {
+      for (int ww = 0; ww < NW; ++ww)
+        for (int h = 0; h < 4; ++h) v += red3[((size_t)(ww * 4 + h) * 4 + (j - jv)) * 16 + c];
+    }
+    out[(size_t)c * A.PW + 1 + j] = v;
+  }
+  if (tid < 2 * C) {
+    const int c = tid >> 1, kind = tid & 1;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww)
+      for (int h = 0; h < 4; ++h) v += red2[(size_t)(ww * 64 + h * 16 + c) * 2 + kind];
+    out[(size_t)c * A.PW + (kind == 0 ? D + 1 : 0)] = v;
+  }
+}
+
 // v5 sweep: 64 chains of a shard, any d -- two fp64 MFMA GEMM passes (BASELINE configs[4]:
 // full-data logistic regression, d = 1000, 64 chains).
 //
@@ -1683,6 +1919,9 @@ static hipError_t pick_tile(const SweepArgs& A, int64_t n, int d, int T, int nbl
   return hipErrorInvalidValue;
 }
 
+#ifndef STK_SWEEPM_DEFAULT
+#define STK_SWEEPM_DEFAULT 0
+#endif
 template <int FAM>
 static hipError_t launch_sweepm(const SweepArgs& A, int d, int nblocks, size_t lds, hipStream_t st) {
   auto go = [&](auto kern) {
@@ -1690,8 +1929,17 @@ static hipError_t launch_sweepm(const SweepArgs& A, int d, int nblocks, size_t l
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A, A.LD);
     return hipGetLastError();
   };
-  if (d == 100) {                     // early slot release (v4e): 2-3 % over k_sweepm here
-    auto kern = k_sweepe<FAM, 25, 7>;
+  if (d == 100) {
+    // v4r (register-streamed next sub-tile, PF in flight) or v4e (early slot release);
+    // STARK_SWEEPM = e | r | r2 selects one for measurements
+    static const int sel = [] {
+      const char* e = getenv("STARK_SWEEPM");
+      if (e && !strcmp(e, "e")) return 0;
+      if (e && !strcmp(e, "r2")) return 2;
+      if (e && !strcmp(e, "r")) return 1;
+      return STK_SWEEPM_DEFAULT;
+    }();
+    auto kern = sel == 0 ? k_sweepe<FAM, 25, 7> : (sel == 2 ? k_sweepr<FAM, 25, 7, 2> : k_sweepr<FAM, 25, 7, 1>);
     allow_big_lds((const void*)kern);
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A);
     return hipGetLastError();
