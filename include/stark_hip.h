@@ -17,6 +17,7 @@
  *   stk_consensus_products      stark/stark.py:7-21   consensus_avg(J) reducer body
  *   stk_consensus_solve         stark/stark.py:66-70  inv(sum W) . sum W theta
  *   stk_consensus               stark/stark.py:66-70  reduce + solve over all shards
+ *   stk_consensus_blocked       the same with block-diagonal weights (lp__ in its own block)
  *
  * Conventions
  *   - Return 0 on success, a negative STK_E_* code on failure; stk_last_error() gives a
@@ -196,6 +197,11 @@ STK_API int stk_consensus_solve(stk_ctx* ctx, const double* sum_w, const double*
                                 int32_t S, double* out);
 STK_API int stk_consensus(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S, double* out,
                           int32_t* shard_used);
+/* stk_consensus with block-diagonal weights: row_block[a] names the weight block of row a
+ * (e.g. 0 for the parameters, 1 for lp__); covariances between rows of different blocks are
+ * taken as 0, so each block is combined from its own covariance. */
+STK_API int stk_consensus_blocked(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S,
+                                  const int32_t* row_block, double* out, int32_t* shard_used);
 
 #ifdef __cplusplus
 }

@@ -99,6 +99,7 @@ SIGNATURES = [
     ("stk_consensus_products", ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
     ("stk_consensus_solve", ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _vp]),
     ("stk_consensus", ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
+    ("stk_consensus_blocked", ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
 ]
 
 # int (*stk_allreduce_fn)(void* user, double* block, int64_t count, void* stream)

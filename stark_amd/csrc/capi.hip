@@ -34,15 +34,12 @@ hipError_t stk_launch_sweep_reduce(int family, const ShardDev* shards_dev, int s
 hipError_t stk_launch_gen_shard(double* X, double* yd, int32_t* yi, int64_t nrows, int d, int64_t grow0,
                                 uint64_t seed, double alpha, const double* beta, double noise_sigma, int family,
                                 hipStream_t st);
-hipError_t stk_launch_nan_flags(const double* X, int nshards, int64_t per, int32_t* used, hipStream_t st);
-hipError_t stk_launch_center(const double* X, double* Xc, int rows, int P, int S, hipStream_t st);
-hipError_t stk_launch_gemm(bool bt, const double* A, const double* B, double* C, int M, int N, int K, int lda, int ldb,
-                           int ldc, double alpha, double beta, int batch, size_t sA, size_t sB, size_t sC,
-                           hipStream_t st);
-hipError_t stk_launch_gj_inverse(const double* M, double* W, double* Inv, int P, int batch, int32_t* status,
-                                 hipStream_t st);
-hipError_t stk_launch_masked_sum(const double* src, const int32_t* used, int nshards, size_t n, double* dst,
-                                 hipStream_t st);
+hipError_t stk_launch_consensus_products(const double* X, int nshards, int P, int S, const int32_t* blk, double* mean,
+                                         int32_t* rowbad, int32_t* used, int32_t* status, double* cov, double* W,
+                                         double* work, double* sum_w, double* sum_wtheta, hipStream_t st);
+hipError_t stk_launch_consensus_solve(const double* sum_w, const double* sum_wtheta, int P, int S, double* inv_buf,
+                                      double* work, int32_t* status, double* out, hipStream_t st);
+size_t stk_spd_inverse_work_bytes(int P, int batch);
 
 // ---------------------------------------------------------------- errors
 static thread_local char g_err[1024] = "";
@@ -101,7 +98,7 @@ struct stk_ctx {
   bool own_stream = true;     // false: a caller's stream (stk_ctx_create_on_stream), not destroyed here
   int profiling = 0;
   int refs = 1;
-  DevBuf scratch[8];
+  DevBuf scratch[12];
 };
 
 struct stk_model {
@@ -976,71 +973,101 @@ int stk_transition(stk_model* m, int shard, double* q, int32_t C, uint64_t seed,
 }
 
 // ---------------------------------------------------------------- consensus combine
-int stk_consensus_products(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S, double* sum_w,
-                           double* sum_wtheta, int32_t* shard_used) {
-  ARG_CHECK(ctx && draws && nshards > 0 && P > 0 && S > 1, "stk_consensus_products: bad arguments");
-  ARG_CHECK(P <= 4096, "P = %d too large", P);
-  STK_HIP_CHECK(hipSetDevice(ctx->device));
-  hipStream_t st = ctx->stream;
-  const size_t per = (size_t)P * S;
+// Device buffers of one combine (ctx scratch 8..11): the whole chain runs on the context's
+// stream with one host synchronisation at the end (combine.hip header).
+namespace {
+struct CombineBufs {
+  double *X, *mean, *cov, *W, *work, *sw, *swt, *inv, *out;
+  int32_t *rowbad, *used, *status, *blk;
+};
+int combine_bufs(stk_ctx* ctx, int nshards, int P, int S, CombineBufs* b) {
   DevBuf* B = ctx->scratch;
-  RC(B[0].ensure(sizeof(double) * per * nshards));                   // draws on device
-  RC(B[1].ensure(sizeof(double) * per * nshards));                   // centred, later W theta
-  RC(B[2].ensure(sizeof(double) * (size_t)P * P * nshards));         // cov
-  RC(B[3].ensure(sizeof(double) * (size_t)P * P * nshards));         // W = inv(cov)
-  RC(B[4].ensure(sizeof(double) * (size_t)P * 2 * P * nshards));     // GJ workspace
-  RC(B[5].ensure(sizeof(int32_t) * 2 * nshards + 64));               // used, status
-  RC(B[6].ensure(sizeof(double) * ((size_t)P * P + per)));           // sums
-  double* X = B[0].as<double>();
-  STK_HIP_CHECK(hipMemcpyAsync(X, draws, sizeof(double) * per * nshards, hipMemcpyDefault, st));
-  int32_t* used = B[5].as<int32_t>();
-  int32_t* status = used + nshards;
-  STK_HIP_CHECK(stk_launch_nan_flags(X, nshards, (int64_t)per, used, st));
-  STK_HIP_CHECK(stk_launch_center(X, B[1].as<double>(), nshards * P, P, S, st));
-  // cov_s = Xc_s Xc_s^T * (1/(S-1))     (np.cov: dot(X, X.T) * (1/fact))
-  STK_HIP_CHECK(stk_launch_gemm(true, B[1].as<double>(), B[1].as<double>(), B[2].as<double>(), P, P, S, S, S, P,
-                                1.0 / (double)(S - 1), 0.0, nshards, per, per, (size_t)P * P, st));
-  STK_HIP_CHECK(stk_launch_gj_inverse(B[2].as<double>(), B[4].as<double>(), B[3].as<double>(), P, nshards, status, st));
-  // W_s theta_s into B[1]
-  STK_HIP_CHECK(stk_launch_gemm(false, B[3].as<double>(), X, B[1].as<double>(), P, S, P, P, S, S, 1.0, 0.0, nshards,
-                                (size_t)P * P, per, per, st));
-  std::vector<int32_t> hu(2 * nshards);
-  STK_HIP_CHECK(hipMemcpyAsync(hu.data(), used, sizeof(int32_t) * 2 * nshards, hipMemcpyDeviceToHost, st));
-  STK_HIP_CHECK(hipStreamSynchronize(st));
+  const size_t per = (size_t)P * S, pp = (size_t)P * P;
+  const size_t wk = stk_spd_inverse_work_bytes(P, nshards);
+  RC(B[8].ensure(sizeof(double) * (per * nshards + per * 2 + (size_t)P * nshards)));
+  RC(B[9].ensure(sizeof(double) * (pp * nshards * 2 + pp * 2) + wk + 16));
+  RC(B[10].ensure(sizeof(int32_t) * ((size_t)P * nshards + 2 * (size_t)nshards + 2 + (size_t)P) + 64));
+  b->X = B[8].as<double>();
+  b->swt = b->X + per * nshards;
+  b->out = b->swt + per;
+  b->mean = b->out + per;
+  b->cov = B[9].as<double>();
+  b->W = b->cov + pp * nshards;
+  b->sw = b->W + pp * nshards;
+  b->inv = b->sw + pp;
+  b->work = b->inv + pp;
+  b->rowbad = B[10].as<int32_t>();
+  b->used = b->rowbad + (size_t)P * nshards;
+  b->status = b->used + nshards;               // nshards + 1 (the last: the final solve)
+  b->blk = b->status + nshards + 1;
+  return STK_OK;
+}
+// host-side outcome of a products run: LinAlgError / all-NaN
+int combine_check(const std::vector<int32_t>& h, int nshards, int32_t* shard_used) {
   int nused = 0;
   for (int s = 0; s < nshards; ++s) {
-    if (hu[s] && hu[nshards + s]) {
+    if (h[s] && h[nshards + s]) {
       stk_set_error("shard %d: singular sample covariance (LinAlgError)", s);
       return STK_E_LINALG;
     }
-    nused += hu[s];
-    if (shard_used) shard_used[s] = hu[s];
+    nused += h[s];
+    if (shard_used) shard_used[s] = h[s];
   }
   if (nused == 0) {
     stk_set_error("every shard holds NaN draws");
     return STK_E_NAN;
   }
-  double* sw = B[6].as<double>();
-  double* swt = sw + (size_t)P * P;
-  STK_HIP_CHECK(stk_launch_masked_sum(B[3].as<double>(), used, nshards, (size_t)P * P, sw, st));
-  STK_HIP_CHECK(stk_launch_masked_sum(B[1].as<double>(), used, nshards, per, swt, st));
-  if (sum_w) STK_HIP_CHECK(hipMemcpyAsync(sum_w, sw, sizeof(double) * P * P, hipMemcpyDefault, st));
-  if (sum_wtheta) STK_HIP_CHECK(hipMemcpyAsync(sum_wtheta, swt, sizeof(double) * per, hipMemcpyDefault, st));
+  return STK_OK;
+}
+int consensus_run(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S, const int32_t* row_block,
+                  double* sum_w, double* sum_wtheta, double* out, int32_t* shard_used) {
+  ARG_CHECK(ctx && draws && nshards > 0 && P > 0 && S > 1, "stk_consensus: bad arguments");
+  ARG_CHECK(P <= 4096, "P = %d too large", P);
+  STK_HIP_CHECK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const size_t per = (size_t)P * S;
+  CombineBufs b;
+  RC(combine_bufs(ctx, nshards, P, S, &b));
+  STK_HIP_CHECK(hipMemcpyAsync(b.X, draws, sizeof(double) * per * nshards, hipMemcpyDefault, st));
+  if (row_block) STK_HIP_CHECK(hipMemcpyAsync(b.blk, row_block, sizeof(int32_t) * P, hipMemcpyDefault, st));
+  STK_HIP_CHECK(stk_launch_consensus_products(b.X, nshards, P, S, row_block ? b.blk : nullptr, b.mean, b.rowbad,
+                                              b.used, b.status, b.cov, b.W, b.work, b.sw, b.swt, st));
+  if (out) STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status + nshards, b.out, st));
+  std::vector<int32_t> h(2 * nshards + 1, 0);
+  STK_HIP_CHECK(hipMemcpyAsync(h.data(), b.used, sizeof(int32_t) * (2 * nshards + (out ? 1 : 0)), hipMemcpyDeviceToHost, st));
+  STK_HIP_CHECK(hipStreamSynchronize(st));
+  RC(combine_check(h, nshards, shard_used));
+  if (out && h[2 * nshards]) {
+    stk_set_error("singular sum of weights (LinAlgError)");
+    return STK_E_LINALG;
+  }
+  if (sum_w) STK_HIP_CHECK(hipMemcpyAsync(sum_w, b.sw, sizeof(double) * P * P, hipMemcpyDefault, st));
+  if (sum_wtheta) STK_HIP_CHECK(hipMemcpyAsync(sum_wtheta, b.swt, sizeof(double) * per, hipMemcpyDefault, st));
+  if (out) STK_HIP_CHECK(hipMemcpyAsync(out, b.out, sizeof(double) * per, hipMemcpyDefault, st));
   STK_HIP_CHECK(hipStreamSynchronize(st));
   return STK_OK;
 }
+}  // namespace
 
-static int solve_on_device(stk_ctx* ctx, const double* sw, const double* swt, int P, int S, double* out_dev) {
+int stk_consensus_products(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S, double* sum_w,
+                           double* sum_wtheta, int32_t* shard_used) {
+  return consensus_run(ctx, draws, nshards, P, S, nullptr, sum_w, sum_wtheta, nullptr, shard_used);
+}
+
+int stk_consensus_solve(stk_ctx* ctx, const double* sum_w, const double* sum_wtheta, int32_t P, int32_t S,
+                        double* out) {
+  ARG_CHECK(ctx && sum_w && sum_wtheta && out && P > 0 && S > 0, "stk_consensus_solve: bad arguments");
+  STK_HIP_CHECK(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
-  DevBuf* B = ctx->scratch;
-  RC(B[7].ensure(sizeof(double) * ((size_t)P * P * 2 + (size_t)P * 2 * P) + 64));
-  double* inv = B[7].as<double>();
-  double* work = inv + (size_t)P * P;
-  int32_t* status = (int32_t*)(work + (size_t)P * 2 * P + (size_t)P * P);
-  STK_HIP_CHECK(stk_launch_gj_inverse(sw, work, inv, P, 1, status, st));
+  const size_t per = (size_t)P * S;
+  CombineBufs b;
+  RC(combine_bufs(ctx, 1, P, S, &b));
+  STK_HIP_CHECK(hipMemcpyAsync(b.sw, sum_w, sizeof(double) * P * P, hipMemcpyDefault, st));
+  STK_HIP_CHECK(hipMemcpyAsync(b.swt, sum_wtheta, sizeof(double) * per, hipMemcpyDefault, st));
+  STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status, b.out, st));
   int32_t hs = 0;
-  STK_HIP_CHECK(hipMemcpyAsync(&hs, status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-  STK_HIP_CHECK(stk_launch_gemm(false, inv, swt, out_dev, P, S, P, P, S, S, 1.0, 0.0, 1, 0, 0, 0, st));
+  STK_HIP_CHECK(hipMemcpyAsync(&hs, b.status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  STK_HIP_CHECK(hipMemcpyAsync(out, b.out, sizeof(double) * per, hipMemcpyDefault, st));
   STK_HIP_CHECK(hipStreamSynchronize(st));
   if (hs) {
     stk_set_error("singular sum of weights (LinAlgError)");
@@ -1049,39 +1076,16 @@ static int solve_on_device(stk_ctx* ctx, const double* sw, const double* swt, in
   return STK_OK;
 }
 
-int stk_consensus_solve(stk_ctx* ctx, const double* sum_w, const double* sum_wtheta, int32_t P, int32_t S,
-                        double* out) {
-  ARG_CHECK(ctx && sum_w && sum_wtheta && out && P > 0 && S > 0, "stk_consensus_solve: bad arguments");
-  STK_HIP_CHECK(hipSetDevice(ctx->device));
-  hipStream_t st = ctx->stream;
-  DevBuf* B = ctx->scratch;
-  const size_t per = (size_t)P * S;
-  RC(B[6].ensure(sizeof(double) * ((size_t)P * P + 2 * per)));
-  double* sw = B[6].as<double>();
-  double* swt = sw + (size_t)P * P;
-  double* o = swt + per;
-  STK_HIP_CHECK(hipMemcpyAsync(sw, sum_w, sizeof(double) * P * P, hipMemcpyDefault, st));
-  STK_HIP_CHECK(hipMemcpyAsync(swt, sum_wtheta, sizeof(double) * per, hipMemcpyDefault, st));
-  RC(solve_on_device(ctx, sw, swt, P, S, o));
-  STK_HIP_CHECK(hipMemcpyAsync(out, o, sizeof(double) * per, hipMemcpyDefault, st));
-  STK_HIP_CHECK(hipStreamSynchronize(st));
-  return STK_OK;
-}
-
 int stk_consensus(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S, double* out,
                   int32_t* shard_used) {
   ARG_CHECK(out, "stk_consensus: out is NULL");
-  RC(stk_consensus_products(ctx, draws, nshards, P, S, nullptr, nullptr, shard_used));
-  hipStream_t st = ctx->stream;
-  DevBuf* B = ctx->scratch;
-  const size_t per = (size_t)P * S;
-  double* sw = B[6].as<double>();
-  double* swt = sw + (size_t)P * P;
-  // reuse B[1] (W theta, no longer needed) as the output
-  RC(solve_on_device(ctx, sw, swt, P, S, B[1].as<double>()));
-  STK_HIP_CHECK(hipMemcpyAsync(out, B[1].p, sizeof(double) * per, hipMemcpyDefault, st));
-  STK_HIP_CHECK(hipStreamSynchronize(st));
-  return STK_OK;
+  return consensus_run(ctx, draws, nshards, P, S, nullptr, nullptr, nullptr, out, shard_used);
+}
+
+int stk_consensus_blocked(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S,
+                          const int32_t* row_block, double* out, int32_t* shard_used) {
+  ARG_CHECK(out && row_block, "stk_consensus_blocked: out / row_block is NULL");
+  return consensus_run(ctx, draws, nshards, P, S, row_block, nullptr, nullptr, out, shard_used);
 }
 
 }  // extern "C"

@@ -4,89 +4,215 @@
 // [sum W_s, sum W_s theta_s]) and the driver solve stark/stark.py:66-70
 // (inv(sum W) . sum W theta).  General in the shard count (the reference reducer only
 // works for two partitions); shards holding NaN draws are left out, the
-// intent of the guard at stark/stark.py:9-10.  All sums run in shard order, so the result
-// is bitwise identical however the shards were spread over GPUs.
+// intent of the guard at stark/stark.py:9-10.  Every sum runs in a fixed order, so the
+// result is bitwise identical however the shards were spread over GPUs.
 //
-// Kernels: per-row means, centring, a 16x16-tiled fp64 GEMM (LDS-staged K slices) for
-// cov = Xc Xc^T * 1/(S-1), W_s theta_s and the final product, and Gauss-Jordan inversion
-// with partial pivoting (one workgroup per matrix, as LAPACK getrf+getri pivot rows).
+// The whole combine is a handful of launches on one stream, no host round trip in between:
+//   k_row_stats      per (shard, row): mean over the S draws (np.cov centres rows) + NaN flag
+//   k_gemm64<Cov>    cov_s = (X_s - m_s)(X_s - m_s)^T / (S - 1), centring folded into the
+//                    tile loads; rows of different weight blocks (lp__ alone)
+//                    get 0, so the weights are block-diagonal when asked for
+//   k_spd_inverse    W_s = inv(cov_s): in-place Gauss-Jordan on the matrix held in LDS
+//                    (P <= 128: 128 KB of the CU's 160), diagonal pivots -- a covariance is
+//                    symmetric positive (semi)definite, where diagonal pivoting is stable
+//                    (Cholesky's argument); a pivot <= 0 or NaN is reported as singular
+//                    (LinAlgError).  One workgroup per shard, shards in parallel.  P > 128
+//                    falls back to k_gj_inverse (partial pivoting, global memory).
+//   k_sum_w          sum_s W_s in shard order (NaN shards hold W = 0)
+//   k_gemm64<WTheta> sum_s W_s theta_s as ONE GEMM with K = shards x P:
+//                    [W_1 .. W_S] (P x SP) . [theta_1; ..; theta_S] (SP x S), NaN shards skipped
+//   k_spd_inverse + k_gemm64<Plain>  out = inv(sum W) . sum W theta
+// k_gemm64: 64 x 64 output tile per 256-thread block, 4 x 4 outputs per thread (rows
+// ty + 16 i, columns tx + 16 j), 16-deep K slices staged in LDS; each output sums its K
+// terms in index order.
 #include "common.h"
 #include <math.h>
+#include <algorithm>
 
 namespace stk {
 
-__global__ __launch_bounds__(256) void k_nan_flags(const double* X, int64_t per, int32_t* used) {
-  const int s = blockIdx.x;
-  const double* x = X + (size_t)s * per;
-  int bad = 0;
-  for (int64_t i = threadIdx.x; i < per; i += blockDim.x) bad |= isnan(x[i]) ? 1 : 0;
-  bad = __syncthreads_or(bad);
-  if (threadIdx.x == 0) used[s] = bad ? 0 : 1;
+constexpr int CB_T = 64;     // output tile
+constexpr int CB_K = 16;     // K slice
+
+// ---- tile loaders: a(m, k), b(k, n), store(m, n, v)
+struct CovLd {               // batch = shard (blockIdx.z)
+  const double* X;           // [shard][P][S]
+  const double* mean;        // [shard][P]
+  const int32_t* blk;        // [P] weight block of each row, or null (one block)
+  double* cov;               // [shard][P][P]
+  int P, S;
+  double scale;
+  __device__ double a(int z, int m, int k) const { return X[((size_t)z * P + m) * S + k] - mean[(size_t)z * P + m]; }
+  __device__ double b(int z, int k, int n) const { return X[((size_t)z * P + n) * S + k] - mean[(size_t)z * P + n]; }
+  __device__ void store(int z, int m, int n, double v) const {
+    cov[((size_t)z * P + m) * P + n] = (blk && blk[m] != blk[n]) ? 0.0 : v * scale;
+  }
+};
+struct WThetaLd {            // sum_s W_s theta_s, K = nshards * P
+  const double* W;           // [shard][P][P]
+  const double* X;           // [shard][P][S] = [(shard, row)][S]
+  const int32_t* used;       // [shard]
+  double* out;               // [P][S]
+  int P, S;
+  __device__ double a(int, int m, int k) const {
+    const int s = k / P;
+    return used[s] ? W[((size_t)s * P + m) * P + (k - s * P)] : 0.0;
+  }
+  __device__ double b(int, int k, int n) const { return used[k / P] ? X[(size_t)k * S + n] : 0.0; }
+  __device__ void store(int, int m, int n, double v) const { out[(size_t)m * S + n] = v; }
+};
+struct PlainLd {             // C[M x N] = A[M x K] . B[K x N], row-major
+  const double* A;
+  const double* B;
+  double* C;
+  int lda, ldb, ldc;
+  __device__ double a(int, int m, int k) const { return A[(size_t)m * lda + k]; }
+  __device__ double b(int, int k, int n) const { return B[(size_t)k * ldb + n]; }
+  __device__ void store(int, int m, int n, double v) const { C[(size_t)m * ldc + n] = v; }
+};
+
+template <class LD>
+__global__ __launch_bounds__(256) void k_gemm64(LD L, int M, int N, int K) {
+  __shared__ double As[CB_K][CB_T + 1];
+  __shared__ double Bs[CB_K][CB_T + 1];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int m0 = blockIdx.y * CB_T, n0 = blockIdx.x * CB_T, z = blockIdx.z;
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  for (int k0 = 0; k0 < K; k0 += CB_K) {
+    // A slice: 64 rows x 16 k (consecutive threads: consecutive k of a row)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = threadIdx.x + 256 * r;
+      const int mm = e >> 4, kk = e & 15;
+      const int m = m0 + mm, k = k0 + kk;
+      As[kk][mm] = (m < M && k < K) ? L.a(z, m, k) : 0.0;
+    }
+    // B slice: 16 k x 64 columns (consecutive threads: consecutive columns)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = threadIdx.x + 256 * r;
+      const int kk = e >> 6, nn = e & 63;
+      const int n = n0 + nn, k = k0 + kk;
+      Bs[kk][nn] = (n < N && k < K) ? L.b(z, k, n) : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < CB_K; ++kk) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = As[kk][ty + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = Bs[kk][tx + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fma(av[i], bv[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + ty + 16 * i, n = n0 + tx + 16 * j;
+      if (m < M && n < N) L.store(z, m, n, acc[i][j]);
+    }
 }
 
-// mean over the S columns of row (s, a), then centred copy (numpy: X -= X.mean(axis=1)).
-__global__ __launch_bounds__(256) void k_center(const double* X, double* Xc, int P, int S) {
-  const int row = blockIdx.x;   // s * P + a
+// per (shard, row): mean over S (fixed-order block sum) and a NaN flag
+__global__ __launch_bounds__(256) void k_row_stats(const double* X, int S, double* mean, int32_t* rowbad) {
+  const int row = blockIdx.x;
   const double* x = X + (size_t)row * S;
-  double* xc = Xc + (size_t)row * S;
   __shared__ double red[256];
   double v = 0.0;
-  for (int k = threadIdx.x; k < S; k += 256) v += x[k];
+  int bad = 0;
+  for (int k = threadIdx.x; k < S; k += 256) {
+    const double t = x[k];
+    bad |= isnan(t) ? 1 : 0;
+    v += t;
+  }
   red[threadIdx.x] = v;
-  __syncthreads();
+  bad = __syncthreads_or(bad);
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  const double mean = red[0] / (double)S;
-  for (int k = threadIdx.x; k < S; k += 256) xc[k] = x[k] - mean;
+  if (threadIdx.x == 0) {
+    mean[row] = red[0] / (double)S;
+    rowbad[row] = bad;
+  }
 }
 
-// C[M x N] (ldc) = alpha * A[M x K] (lda) . op(B) + beta * C, op(B) = B[K x N] or B^T with
-// B stored [N x K].  batch over blockIdx.z with strides.  16x16 threads, 16-deep K slices.
-template <bool BT>
-__global__ __launch_bounds__(256) void k_gemm(const double* A, const double* B, double* C, int M, int N, int K,
-                                              int lda, int ldb, int ldc, double alpha, double beta, size_t sA,
-                                              size_t sB, size_t sC) {
-  __shared__ double As[16][17];
-  __shared__ double Bs[16][17];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int row = blockIdx.y * 16 + ty, col = blockIdx.x * 16 + tx;
-  A += sA * blockIdx.z;
-  B += sB * blockIdx.z;
-  C += sC * blockIdx.z;
-  double acc = 0.0;
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    const int ar = blockIdx.y * 16 + ty, ak = k0 + tx;
-    As[ty][tx] = (ar < M && ak < K) ? A[(size_t)ar * lda + ak] : 0.0;
-    if (BT) {
-      const int bn = blockIdx.x * 16 + ty, bk = k0 + tx;   // B is [N x K]
-      Bs[tx][ty] = (bn < N && bk < K) ? B[(size_t)bn * ldb + bk] : 0.0;
-    } else {
-      const int bk = k0 + ty, bn = blockIdx.x * 16 + tx;   // B is [K x N]
-      Bs[ty][tx] = (bk < K && bn < N) ? B[(size_t)bk * ldb + bn] : 0.0;
+// used[s] = no NaN in any of its P rows
+__global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t* used) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nshards) return;
+  int bad = 0;
+  for (int a = 0; a < P; ++a) bad |= rowbad[(size_t)s * P + a];
+  used[s] = bad ? 0 : 1;
+}
+
+// In-place Gauss-Jordan inverse of a batch of SPD P x P matrices held in LDS (stride P + 1).
+// Shard b with used[b] == 0 (NaN draws) gets W = 0 and no status.  status[b] = 1 when a
+// pivot is <= 0 or NaN (a singular covariance: numpy's inv raises LinAlgError).
+__global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
+                                                      int32_t* status) {
+  extern __shared__ double A[];   // [P][P + 1], then row k [P], column k [P]
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, LDA = P + 1;
+  const double* M = Min + (size_t)b * P * P;
+  double* out = Out + (size_t)b * P * P;
+  if (used && !used[b]) {
+    for (int i = tid; i < P * P; i += nt) out[i] = 0.0;
+    if (tid == 0) status[b] = 0;
+    return;
+  }
+  double* rowk = A + (size_t)P * LDA;
+  double* colk = rowk + P;
+  for (int i = tid; i < P * P; i += nt) A[(i / P) * LDA + i % P] = M[i];
+  __syncthreads();
+  int sing = 0;
+  for (int k = 0; k < P; ++k) {
+    const double piv = A[k * LDA + k];
+    if (!(piv > 0.0)) { sing = 1; break; }      // uniform: every thread read the same pivot
+    const double ip = 1.0 / piv;
+    for (int i = tid; i < P; i += nt) {
+      rowk[i] = A[k * LDA + i] * ip;
+      colk[i] = A[i * LDA + k];
     }
     __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) acc += As[ty][kk] * Bs[kk][tx];
+    for (int e = tid; e < P * P; e += nt) {
+      const int i = e / P, j = e % P;
+      double v;
+      if (i == k) v = (j == k) ? ip : rowk[j];
+      else if (j == k) v = -colk[i] * ip;
+      else v = fma(-colk[i], rowk[j], A[i * LDA + j]);
+      A[i * LDA + j] = v;
+    }
     __syncthreads();
   }
-  if (row < M && col < N) {
-    double* c = C + (size_t)row * ldc + col;
-    *c = (beta == 0.0) ? alpha * acc : alpha * acc + beta * *c;
-  }
+  for (int i = tid; i < P * P; i += nt) out[i] = A[(i / P) * LDA + i % P];
+  if (tid == 0) status[b] = sing;
 }
 
-// Gauss-Jordan inverse with partial pivoting of a batch of P x P matrices.  W holds the
-// [P x 2P] augmented workspace per matrix; writes the inverse to Inv.  status[b] = 1 on a
-// zero pivot (singular).
+// Gauss-Jordan inverse with partial pivoting of a batch of P x P matrices in global memory
+// (P > 128).  W holds the [P x 2P] augmented workspace per matrix; status[b] = 1 on a zero
+// pivot.  Shards with used[b] == 0 get W = 0.
 __global__ __launch_bounds__(1024) void k_gj_inverse(const double* Min, double* W, double* Inv, int P,
-                                                     int32_t* status) {
+                                                     const int32_t* used, int32_t* status) {
   const int b = blockIdx.x;
   const double* M = Min + (size_t)b * P * P;
   double* A = W + (size_t)b * P * 2 * P;
   double* out = Inv + (size_t)b * P * P;
   const int tid = threadIdx.x, nt = blockDim.x, W2 = 2 * P;
+  if (used && !used[b]) {
+    for (int i = tid; i < P * P; i += nt) out[i] = 0.0;
+    if (tid == 0) status[b] = 0;
+    return;
+  }
   for (int i = tid; i < P * W2; i += nt) {
     const int r = i / W2, c = i % W2;
     A[i] = c < P ? M[(size_t)r * P + c] : (c - P == r ? 1.0 : 0.0);
@@ -97,7 +223,6 @@ __global__ __launch_bounds__(1024) void k_gj_inverse(const double* Min, double* 
   if (tid == 0) singular = 0;
   __syncthreads();
   for (int k = 0; k < P; ++k) {
-    // pivot search over rows k..P-1 (max |a_ik|, lowest index on ties)
     double best = -1.0;
     int bi = k;
     for (int i = k + tid; i < P; i += nt) {
@@ -132,10 +257,8 @@ __global__ __launch_bounds__(1024) void k_gj_inverse(const double* Min, double* 
     __syncthreads();
     for (int i = tid; i < P * W2; i += nt) {
       const int r = i / W2, c = i % W2;
-      if (r == k) continue;
-      const double f = A[(size_t)r * W2 + k];
-      if (c == k) continue;
-      A[i] -= f * A[(size_t)k * W2 + c];
+      if (r == k || c == k) continue;
+      A[i] -= A[(size_t)r * W2 + k] * A[(size_t)k * W2 + c];
     }
     __syncthreads();
     for (int r = tid; r < P; r += nt)
@@ -149,55 +272,69 @@ __global__ __launch_bounds__(1024) void k_gj_inverse(const double* Min, double* 
   if (tid == 0) status[b] = singular;
 }
 
-// sum over used shards, in shard order: dst = sum_s src_s (n elements each)
-__global__ void k_masked_sum(const double* src, const int32_t* used, int nshards, size_t n, double* dst) {
+// sum over shards, in shard order (NaN shards hold zeros): dst = sum_s src_s
+__global__ void k_sum_w(const double* src, int nshards, size_t n, double* dst) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    double v = 0.0;
-    bool any = false;
-    for (int s = 0; s < nshards; ++s) {
-      if (!used[s]) continue;
-      const double x = src[(size_t)s * n + i];
-      v = any ? v + x : x;
-      any = true;
-    }
+    double v = src[i];
+    for (int s = 1; s < nshards; ++s) v += src[(size_t)s * n + i];
     dst[i] = v;
   }
+}
+
+template <class LD>
+static hipError_t gemm64(const LD& L, int M, int N, int K, int batch, hipStream_t st) {
+  dim3 grid((N + CB_T - 1) / CB_T, (M + CB_T - 1) / CB_T, batch);
+  hipLaunchKernelGGL(k_gemm64<LD>, grid, dim3(256), 0, st, L, M, N, K);
+  return hipGetLastError();
 }
 
 }  // namespace stk
 
 using namespace stk;
 
-hipError_t stk_launch_nan_flags(const double* X, int nshards, int64_t per, int32_t* used, hipStream_t st) {
-  hipLaunchKernelGGL(k_nan_flags, dim3(nshards), dim3(256), 0, st, X, per, used);
+static bool lds_inverse_fits(int P) { return P <= 128; }
+
+// batched inverse of SPD matrices (workspace only for P > 128)
+hipError_t stk_launch_spd_inverse(const double* M, double* Inv, double* work, int P, int batch, const int32_t* used,
+                                  int32_t* status, hipStream_t st) {
+  if (lds_inverse_fits(P)) {
+    const size_t lds = sizeof(double) * ((size_t)P * (P + 1) + 2 * (size_t)P);
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)k_spd_inverse, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    const int nt = P <= 32 ? 256 : 1024;
+    hipLaunchKernelGGL(k_spd_inverse, dim3(batch), dim3(nt), lds, st, M, Inv, P, used, status);
+  } else {
+    hipLaunchKernelGGL(k_gj_inverse, dim3(batch), dim3(1024), 0, st, M, work, Inv, P, used, status);
+  }
   return hipGetLastError();
 }
-hipError_t stk_launch_center(const double* X, double* Xc, int rows, int P, int S, hipStream_t st) {
-  hipLaunchKernelGGL(k_center, dim3(rows), dim3(256), 0, st, X, Xc, P, S);
-  return hipGetLastError();
+size_t stk_spd_inverse_work_bytes(int P, int batch) {
+  return lds_inverse_fits(P) ? 0 : sizeof(double) * (size_t)P * 2 * P * batch;
 }
-hipError_t stk_launch_gemm(bool bt, const double* A, const double* B, double* C, int M, int N, int K, int lda, int ldb,
-                           int ldc, double alpha, double beta, int batch, size_t sA, size_t sB, size_t sC,
-                           hipStream_t st) {
-  dim3 grid((N + 15) / 16, (M + 15) / 16, batch);
-  if (bt)
-    hipLaunchKernelGGL(k_gemm<true>, grid, dim3(256), 0, st, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, sA, sB, sC);
-  else
-    hipLaunchKernelGGL(k_gemm<false>, grid, dim3(256), 0, st, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, sA, sB, sC);
-  return hipGetLastError();
+
+// draws X [nshards][P][S] on the device -> W [nshards][P][P], sum_w [P][P], sum_wtheta [P][S].
+hipError_t stk_launch_consensus_products(const double* X, int nshards, int P, int S, const int32_t* blk, double* mean,
+                                         int32_t* rowbad, int32_t* used, int32_t* status, double* cov, double* W,
+                                         double* work, double* sum_w, double* sum_wtheta, hipStream_t st) {
+  hipLaunchKernelGGL(k_row_stats, dim3(nshards * P), dim3(256), 0, st, X, S, mean, rowbad);
+  hipLaunchKernelGGL(k_shard_used, dim3((nshards + 63) / 64), dim3(64), 0, st, rowbad, P, nshards, used);
+  hipError_t e = gemm64(CovLd{X, mean, blk, cov, P, S, 1.0 / (double)(S - 1)}, P, P, S, nshards, st);
+  if (e != hipSuccess) return e;
+  e = stk_launch_spd_inverse(cov, W, work, P, nshards, used, status, st);
+  if (e != hipSuccess) return e;
+  const size_t pp = (size_t)P * P;
+  hipLaunchKernelGGL(k_sum_w, dim3((unsigned)std::min<size_t>((pp + 255) / 256, 1024)), dim3(256), 0, st, W, nshards,
+                     pp, sum_w);
+  return gemm64(WThetaLd{W, X, used, sum_wtheta, P, S}, P, S, nshards * P, 1, st);
 }
-hipError_t stk_launch_gj_inverse(const double* M, double* W, double* Inv, int P, int batch, int32_t* status,
-                                 hipStream_t st) {
-  int nt = 256;
-  while (nt < 1024 && nt < 2 * P) nt *= 2;
-  hipLaunchKernelGGL(k_gj_inverse, dim3(batch), dim3(nt), 0, st, M, W, Inv, P, status);
-  return hipGetLastError();
-}
-hipError_t stk_launch_masked_sum(const double* src, const int32_t* used, int nshards, size_t n, double* dst,
-                                 hipStream_t st) {
-  size_t blocks = (n + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks == 0) blocks = 1;
-  hipLaunchKernelGGL(k_masked_sum, dim3((unsigned)blocks), dim3(256), 0, st, src, used, nshards, n, dst);
-  return hipGetLastError();
+
+// out [P][S] = inv(sum_w) . sum_wtheta (inv_buf [P][P], work for P > 128)
+hipError_t stk_launch_consensus_solve(const double* sum_w, const double* sum_wtheta, int P, int S, double* inv_buf,
+                                      double* work, int32_t* status, double* out, hipStream_t st) {
+  hipError_t e = stk_launch_spd_inverse(sum_w, inv_buf, work, P, 1, nullptr, status, st);
+  if (e != hipSuccess) return e;
+  return gemm64(PlainLd{inv_buf, sum_wtheta, out, P, S, S}, P, S, P, 1, st);
 }

@@ -412,20 +412,17 @@ def consensus(draws, ctx: Context | None = None, separate_lp: bool = False):
     the joint combine by a multiple of that offset.  Block weights are exact for a Gaussian
     posterior, where lp__ is uncorrelated with the parameters."""
     ctx = ctx or default_context()
-    if separate_lp:
-        d = [np.asarray(x, np.float64) for x in draws]
-        # one NaN mask over the whole rows, so both blocks combine the same shard set
-        keep = [i for i, x in enumerate(d) if not np.isnan(x).any()]
-        used = np.zeros(len(d), bool)
-        used[keep] = True
-        if not keep:
-            consensus(d, ctx)               # raises the library's "every shard holds NaN draws"
-        th, _ = consensus([d[i][:-1] for i in keep], ctx)
-        lp, _ = consensus([d[i][-1:] for i in keep], ctx)
-        return np.vstack([th, lp]), used
     X, (P, S) = _stack(draws)
     out = np.empty((P, S))
     used = np.empty(len(draws), np.int32)
+    if separate_lp:
+        # one call with block-diagonal weights: parameters in block 0, lp__ (last row) in block 1;
+        # the NaN mask is per shard over all rows, so both blocks combine the same shard set
+        blk = np.zeros(P, np.int32)
+        blk[-1] = 1
+        check(_lib.load().stk_consensus_blocked(ctx._h, X.ctypes.data, len(draws), P, S, blk.ctypes.data,
+                                                out.ctypes.data, used.ctypes.data))
+        return out, used.astype(bool)
     check(_lib.load().stk_consensus(ctx._h, X.ctypes.data, len(draws), P, S, out.ctypes.data, used.ctypes.data))
     return out, used.astype(bool)
 
