@@ -71,35 +71,48 @@ struct PlainLd {             // C[M x N] = A[M x K] . B[K x N], row-major
   __device__ void store(int, int m, int n, double v) const { C[(size_t)m * ldc + n] = v; }
 };
 
+// 64 x 64 tile, K range [kb, ke) of this block's split (blockIdx.z = split * batch + z).
+// The next K slice is loaded into registers while the current one is multiplied.  With a
+// partial buffer the raw sums go to partial[split][z][M][N] and k_splitk_reduce adds the
+// splits in split order (so every output's K terms are summed in a fixed order).
 template <class LD>
-__global__ __launch_bounds__(256) void k_gemm64(LD L, int M, int N, int K) {
+__global__ __launch_bounds__(256) void k_gemm64(LD L, int M, int N, int K, int batch, int kchunk, double* partial) {
   __shared__ double As[CB_K][CB_T + 1];
   __shared__ double Bs[CB_K][CB_T + 1];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int m0 = blockIdx.y * CB_T, n0 = blockIdx.x * CB_T, z = blockIdx.z;
+  const int m0 = blockIdx.y * CB_T, n0 = blockIdx.x * CB_T;
+  const int z = blockIdx.z % batch, split = blockIdx.z / batch;
+  const int kb = split * kchunk, ke = min(K, kb + kchunk);
   double acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
-  for (int k0 = 0; k0 < K; k0 += CB_K) {
-    // A slice: 64 rows x 16 k (consecutive threads: consecutive k of a row)
+  double ra[4], rb[4];
+  auto fetch = [&](int k0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 4; ++r) {        // A slice: 64 rows x 16 k
       const int e = threadIdx.x + 256 * r;
-      const int mm = e >> 4, kk = e & 15;
-      const int m = m0 + mm, k = k0 + kk;
-      As[kk][mm] = (m < M && k < K) ? L.a(z, m, k) : 0.0;
+      const int m = m0 + (e >> 4), k = k0 + (e & 15);
+      ra[r] = (m < M && k < ke) ? L.a(z, m, k) : 0.0;
     }
-    // B slice: 16 k x 64 columns (consecutive threads: consecutive columns)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {        // B slice: 16 k x 64 columns
+      const int e = threadIdx.x + 256 * r;
+      const int n = n0 + (e & 63), k = k0 + (e >> 6);
+      rb[r] = (n < N && k < ke) ? L.b(z, k, n) : 0.0;
+    }
+  };
+  if (kb < ke) fetch(kb);
+  for (int k0 = kb; k0 < ke; k0 += CB_K) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int e = threadIdx.x + 256 * r;
-      const int kk = e >> 6, nn = e & 63;
-      const int n = n0 + nn, k = k0 + kk;
-      Bs[kk][nn] = (n < N && k < K) ? L.b(z, k, n) : 0.0;
+      As[e & 15][e >> 4] = ra[r];
+      Bs[e >> 6][e & 63] = rb[r];
     }
     __syncthreads();
+    if (k0 + CB_K < ke) fetch(k0 + CB_K);
 #pragma unroll
     for (int kk = 0; kk < CB_K; ++kk) {
       double av[4], bv[4];
@@ -119,8 +132,23 @@ __global__ __launch_bounds__(256) void k_gemm64(LD L, int M, int N, int K) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + ty + 16 * i, n = n0 + tx + 16 * j;
-      if (m < M && n < N) L.store(z, m, n, acc[i][j]);
+      if (m < M && n < N) {
+        if (partial) partial[(((size_t)split * batch + z) * M + m) * N + n] = acc[i][j];
+        else L.store(z, m, n, acc[i][j]);
+      }
     }
+}
+
+template <class LD>
+__global__ void k_splitk_reduce(LD L, int M, int N, int batch, int splits, const double* partial) {
+  const size_t tot = (size_t)batch * M * N;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    double v = partial[e];
+    for (int sp = 1; sp < splits; ++sp) v += partial[(size_t)sp * tot + e];
+    const int z = (int)(e / ((size_t)M * N));
+    const size_t r = e % ((size_t)M * N);
+    L.store(z, (int)(r / N), (int)(r % N), v);
+  }
 }
 
 // per (shard, row): mean over S (fixed-order block sum) and a NaN flag
@@ -156,45 +184,63 @@ __global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t*
   used[s] = bad ? 0 : 1;
 }
 
-// In-place Gauss-Jordan inverse of a batch of SPD P x P matrices held in LDS (stride P + 1).
-// Shard b with used[b] == 0 (NaN draws) gets W = 0 and no status.  status[b] = 1 when a
-// pivot is <= 0 or NaN (a singular covariance: numpy's inv raises LinAlgError).
+// In-place Gauss-Jordan inverse of a batch of SPD P x P matrices (P <= 128), the matrix held
+// in REGISTERS: 1024 threads = 128 columns x 8 row groups, thread (j, g) owns A[g + 8 r][j],
+// r < 16.  Step k needs row k and column k as they stood after step k-1; the threads owning
+// elements of row / column k+1 publish them into the other half of a double-buffered LDS
+// pair while they update, so each step costs one barrier.  Shard b with used[b] == 0 (NaN
+// draws) gets W = 0 and no status; status[b] = 1 when a pivot is <= 0 or NaN (singular
+// covariance: numpy's inv raises LinAlgError).
+constexpr int SI_R = 16;
 __global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
                                                       int32_t* status) {
-  extern __shared__ double A[];   // [P][P + 1], then row k [P], column k [P]
-  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, LDA = P + 1;
+  __shared__ double rowk[2][128];
+  __shared__ double colk[2][128];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int j = tid & 127, g = tid >> 7;
   const double* M = Min + (size_t)b * P * P;
   double* out = Out + (size_t)b * P * P;
   if (used && !used[b]) {
-    for (int i = tid; i < P * P; i += nt) out[i] = 0.0;
+    for (int i = tid; i < P * P; i += 1024) out[i] = 0.0;
     if (tid == 0) status[b] = 0;
     return;
   }
-  double* rowk = A + (size_t)P * LDA;
-  double* colk = rowk + P;
-  for (int i = tid; i < P * P; i += nt) A[(i / P) * LDA + i % P] = M[i];
+  double a[SI_R];
+#pragma unroll
+  for (int r = 0; r < SI_R; ++r) {
+    const int i = g + 8 * r;
+    a[r] = (i < P && j < P) ? M[(size_t)i * P + j] : 0.0;
+    if (i == 0 && j < P) rowk[0][j] = a[r];
+    if (j == 0 && i < P) colk[0][i] = a[r];
+  }
   __syncthreads();
   int sing = 0;
   for (int k = 0; k < P; ++k) {
-    const double piv = A[k * LDA + k];
+    const int cur = k & 1, nxt = cur ^ 1;
+    const double piv = rowk[cur][k];
     if (!(piv > 0.0)) { sing = 1; break; }      // uniform: every thread read the same pivot
     const double ip = 1.0 / piv;
-    for (int i = tid; i < P; i += nt) {
-      rowk[i] = A[k * LDA + i] * ip;
-      colk[i] = A[i * LDA + k];
-    }
-    __syncthreads();
-    for (int e = tid; e < P * P; e += nt) {
-      const int i = e / P, j = e % P;
-      double v;
-      if (i == k) v = (j == k) ? ip : rowk[j];
-      else if (j == k) v = -colk[i] * ip;
-      else v = fma(-colk[i], rowk[j], A[i * LDA + j]);
-      A[i * LDA + j] = v;
+    const double rj = j < P ? rowk[cur][j] * ip : 0.0;
+#pragma unroll
+    for (int r = 0; r < SI_R; ++r) {
+      const int i = g + 8 * r;
+      if (i < P && j < P) {
+        double v;
+        if (i == k) v = (j == k) ? ip : rj;
+        else if (j == k) v = -colk[cur][i] * ip;
+        else v = fma(-colk[cur][i], rj, a[r]);
+        a[r] = v;
+        if (i == k + 1) rowk[nxt][j] = v;
+        if (j == k + 1) colk[nxt][i] = v;
+      }
     }
     __syncthreads();
   }
-  for (int i = tid; i < P * P; i += nt) out[i] = A[(i / P) * LDA + i % P];
+#pragma unroll
+  for (int r = 0; r < SI_R; ++r) {
+    const int i = g + 8 * r;
+    if (i < P && j < P) out[(size_t)i * P + j] = a[r];
+  }
   if (tid == 0) status[b] = sing;
 }
 
@@ -281,10 +327,23 @@ __global__ void k_sum_w(const double* src, int nshards, size_t n, double* dst) {
   }
 }
 
+// split K so that the grid has >= ~256 blocks of >= 8 slices each (the K loop is latency-bound)
 template <class LD>
-static hipError_t gemm64(const LD& L, int M, int N, int K, int batch, hipStream_t st) {
-  dim3 grid((N + CB_T - 1) / CB_T, (M + CB_T - 1) / CB_T, batch);
-  hipLaunchKernelGGL(k_gemm64<LD>, grid, dim3(256), 0, st, L, M, N, K);
+static hipError_t gemm64(const LD& L, int M, int N, int K, int batch, double* partial, size_t partial_elems,
+                         hipStream_t st) {
+  const int tiles = ((N + CB_T - 1) / CB_T) * ((M + CB_T - 1) / CB_T) * batch;
+  const int slices = (K + CB_K - 1) / CB_K;
+  int splits = std::max(1, std::min(std::min(slices / 8, (256 + tiles - 1) / tiles), 32));
+  if (!partial || (size_t)splits * batch * M * N > partial_elems) splits = 1;
+  const int kchunk = ((slices + splits - 1) / splits) * CB_K;
+  splits = (K + kchunk - 1) / kchunk;
+  dim3 grid((N + CB_T - 1) / CB_T, (M + CB_T - 1) / CB_T, batch * splits);
+  hipLaunchKernelGGL(k_gemm64<LD>, grid, dim3(256), 0, st, L, M, N, K, batch, kchunk, splits > 1 ? partial : nullptr);
+  if (splits > 1) {
+    const size_t tot = (size_t)batch * M * N;
+    hipLaunchKernelGGL(k_splitk_reduce<LD>, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 2048)), dim3(256), 0, st,
+                       L, M, N, batch, splits, partial);
+  }
   return hipGetLastError();
 }
 
@@ -298,14 +357,7 @@ static bool lds_inverse_fits(int P) { return P <= 128; }
 hipError_t stk_launch_spd_inverse(const double* M, double* Inv, double* work, int P, int batch, const int32_t* used,
                                   int32_t* status, hipStream_t st) {
   if (lds_inverse_fits(P)) {
-    const size_t lds = sizeof(double) * ((size_t)P * (P + 1) + 2 * (size_t)P);
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute((const void*)k_spd_inverse, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
-    const int nt = P <= 32 ? 256 : 1024;
-    hipLaunchKernelGGL(k_spd_inverse, dim3(batch), dim3(nt), lds, st, M, Inv, P, used, status);
+    hipLaunchKernelGGL(k_spd_inverse, dim3(batch), dim3(1024), 0, st, M, Inv, P, used, status);
   } else {
     hipLaunchKernelGGL(k_gj_inverse, dim3(batch), dim3(1024), 0, st, M, work, Inv, P, used, status);
   }
@@ -314,27 +366,34 @@ hipError_t stk_launch_spd_inverse(const double* M, double* Inv, double* work, in
 size_t stk_spd_inverse_work_bytes(int P, int batch) {
   return lds_inverse_fits(P) ? 0 : sizeof(double) * (size_t)P * 2 * P * batch;
 }
+// split-K partial sums: up to 32 splits of the largest GEMM of a combine
+size_t stk_combine_partial_elems(int nshards, int P, int S) {
+  return (size_t)32 * std::max((size_t)nshards * P * P, (size_t)P * S);
+}
 
 // draws X [nshards][P][S] on the device -> W [nshards][P][P], sum_w [P][P], sum_wtheta [P][S].
 hipError_t stk_launch_consensus_products(const double* X, int nshards, int P, int S, const int32_t* blk, double* mean,
                                          int32_t* rowbad, int32_t* used, int32_t* status, double* cov, double* W,
-                                         double* work, double* sum_w, double* sum_wtheta, hipStream_t st) {
+                                         double* work, double* sum_w, double* sum_wtheta, double* partial,
+                                         hipStream_t st) {
+  const size_t pe = stk_combine_partial_elems(nshards, P, S);
   hipLaunchKernelGGL(k_row_stats, dim3(nshards * P), dim3(256), 0, st, X, S, mean, rowbad);
   hipLaunchKernelGGL(k_shard_used, dim3((nshards + 63) / 64), dim3(64), 0, st, rowbad, P, nshards, used);
-  hipError_t e = gemm64(CovLd{X, mean, blk, cov, P, S, 1.0 / (double)(S - 1)}, P, P, S, nshards, st);
+  hipError_t e = gemm64(CovLd{X, mean, blk, cov, P, S, 1.0 / (double)(S - 1)}, P, P, S, nshards, partial, pe, st);
   if (e != hipSuccess) return e;
   e = stk_launch_spd_inverse(cov, W, work, P, nshards, used, status, st);
   if (e != hipSuccess) return e;
   const size_t pp = (size_t)P * P;
   hipLaunchKernelGGL(k_sum_w, dim3((unsigned)std::min<size_t>((pp + 255) / 256, 1024)), dim3(256), 0, st, W, nshards,
                      pp, sum_w);
-  return gemm64(WThetaLd{W, X, used, sum_wtheta, P, S}, P, S, nshards * P, 1, st);
+  return gemm64(WThetaLd{W, X, used, sum_wtheta, P, S}, P, S, nshards * P, 1, partial, pe, st);
 }
 
 // out [P][S] = inv(sum_w) . sum_wtheta (inv_buf [P][P], work for P > 128)
 hipError_t stk_launch_consensus_solve(const double* sum_w, const double* sum_wtheta, int P, int S, double* inv_buf,
-                                      double* work, int32_t* status, double* out, hipStream_t st) {
+                                      double* work, int32_t* status, double* out, double* partial, size_t partial_elems,
+                                      hipStream_t st) {
   hipError_t e = stk_launch_spd_inverse(sum_w, inv_buf, work, P, 1, nullptr, status, st);
   if (e != hipSuccess) return e;
-  return gemm64(PlainLd{inv_buf, sum_wtheta, out, P, S, S}, P, S, P, 1, st);
+  return gemm64(PlainLd{inv_buf, sum_wtheta, out, P, S, S}, P, S, P, 1, partial, partial_elems, st);
 }
