@@ -197,7 +197,7 @@ __global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double*
   __shared__ double rowk[2][128];
   __shared__ double colk[2][128];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int j = tid & 127, g = tid >> 7;
+  const int j = tid & 127, g = uniform_int(tid >> 7);   // g: wave-uniform row group
   const double* M = Min + (size_t)b * P * P;
   double* out = Out + (size_t)b * P * P;
   if (used && !used[b]) {
@@ -205,13 +205,15 @@ __global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double*
     if (tid == 0) status[b] = 0;
     return;
   }
+  // padded to 128 x 128 with an identity block: padding rows/columns have zero coupling, so
+  // the P pivot steps leave them untouched and no element needs a bounds test in the loop
   double a[SI_R];
 #pragma unroll
   for (int r = 0; r < SI_R; ++r) {
     const int i = g + 8 * r;
-    a[r] = (i < P && j < P) ? M[(size_t)i * P + j] : 0.0;
-    if (i == 0 && j < P) rowk[0][j] = a[r];
-    if (j == 0 && i < P) colk[0][i] = a[r];
+    a[r] = (i < P && j < P) ? M[(size_t)i * P + j] : (i == j ? 1.0 : 0.0);
+    if (i == 0) rowk[0][j] = a[r];
+    if (j == 0) colk[0][i] = a[r];
   }
   __syncthreads();
   int sing = 0;
@@ -219,20 +221,24 @@ __global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double*
     const int cur = k & 1, nxt = cur ^ 1;
     const double piv = rowk[cur][k];
     if (!(piv > 0.0)) { sing = 1; break; }      // uniform: every thread read the same pivot
-    const double ip = 1.0 / piv;
-    const double rj = j < P ? rowk[cur][j] * ip : 0.0;
+    double ip = __builtin_amdgcn_rcp(piv);      // 1/piv to the last ulp: two Newton steps
+    ip = fma(ip, fma(-piv, ip, 1.0), ip);
+    ip = fma(ip, fma(-piv, ip, 1.0), ip);
+    const double rj = rowk[cur][j] * ip;
+    const bool jk = j == k;
 #pragma unroll
     for (int r = 0; r < SI_R; ++r) {
-      const int i = g + 8 * r;
-      if (i < P && j < P) {
-        double v;
-        if (i == k) v = (j == k) ? ip : rj;
-        else if (j == k) v = -colk[cur][i] * ip;
-        else v = fma(-colk[cur][i], rj, a[r]);
-        a[r] = v;
-        if (i == k + 1) rowk[nxt][j] = v;
-        if (j == k + 1) colk[nxt][i] = v;
-      }
+      const int i = g + 8 * r;                  // wave-uniform
+      const double ci = colk[cur][i];           // broadcast read
+      double v = fma(-ci, rj, a[r]);
+      v = jk ? -ci * ip : v;
+      if (i == k) v = jk ? ip : rj;
+      a[r] = v;
+      if (i == k + 1) rowk[nxt][j] = v;
+    }
+    if (j == k + 1) {
+#pragma unroll
+      for (int r = 0; r < SI_R; ++r) colk[nxt][g + 8 * r] = a[r];
     }
     __syncthreads();
   }

@@ -25,6 +25,8 @@
 //                 loops its own chain for up to max_steps leapfrogs in ONE launch.
 #include "common.h"
 #include <math.h>
+#include <stdlib.h>
+#include <algorithm>
 
 namespace stk {
 
@@ -55,6 +57,30 @@ __device__ __forceinline__ double wave_sum(double v) {
   return (lane_d(v, 0) + lane_d(v, 16)) + (lane_d(v, 32) + lane_d(v, 48));
 }
 
+// Sum over a segment of SEG consecutive lanes (SEG chains' worth of lanes per wave when
+// chains are packed, SEG = 64 / chains per wave): SEG = 64 is wave_sum; SEG = 16 is one DPP
+// row (the row total of wave_sum's first four steps); SEG = 32 adds the partner row.  For
+// D <= SEG the extra rows of wave_sum only add zeros, so the packed sums are bit-identical.
+template <int SEG>
+__device__ __forceinline__ double seg_sum(double v) {
+  if constexpr (SEG == WAVE) {
+    return wave_sum(v);
+  } else {
+    v += nuts_dpp<0xB1>(v);
+    v += nuts_dpp<0x4E>(v);
+    v += nuts_dpp<0x141>(v);
+    v += nuts_dpp<0x140>(v);
+    if constexpr (SEG == 32) v += __shfl_xor(v, 16);
+    return v;
+  }
+}
+// Lane l of this lane's segment, broadcast to the segment.
+template <int SEG>
+__device__ __forceinline__ double seg_bcast(double v, int l) {
+  if constexpr (SEG == WAVE) return lane_d(v, l);
+  else return __shfl(v, ((int)threadIdx.x & (WAVE - SEG)) + l);
+}
+
 __device__ __forceinline__ double log_sum_exp2(double a, double b) {   // stan::math::log_sum_exp
   if (a == -INFINITY) return b;
   if (a == INFINITY && b == INFINITY) return INFINITY;
@@ -65,15 +91,15 @@ __device__ __forceinline__ double log_sum_exp2(double a, double b) {   // stan::
 // ------------------------------------------------------------------ model hooks
 // 8 schools (example/schools.stan:1-18): q = (mu, log tau, eta_1..J); returns lp, writes
 // grad lp.  Mirrors oracle orc_schools_lpgrad.
-template <int NCH>
+template <int NCH, int SEG = WAVE>
 __device__ double schools_lpgrad(const ShardDev& sh, const double (&q)[NCH], double (&glp)[NCH], int lane, int D) {
-  const double mu = lane_d(q[0], 0);
-  const double u = lane_d(q[0], 1);
+  const double mu = seg_bcast<SEG>(q[0], 0);
+  const double u = seg_bcast<SEG>(q[0], 1);
   const double tau = exp(u);
   double lp = 0.0, smu = 0.0, su = 0.0;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
-    const int e = k * WAVE + lane;
+    const int e = k * SEG + lane;
     glp[k] = 0.0;
     if (e >= 2 && e < D) {
       const int j = e - 2;
@@ -88,34 +114,34 @@ __device__ double schools_lpgrad(const ShardDev& sh, const double (&q)[NCH], dou
       glp[k] = -eta + tau * r;
     }
   }
-  lp = wave_sum(lp) + u;
-  smu = wave_sum(smu);
-  su = wave_sum(su);
+  lp = seg_sum<SEG>(lp) + u;
+  smu = seg_sum<SEG>(smu);
+  su = seg_sum<SEG>(su);
   if (lane == 0) glp[0] = smu;
   if (lane == 1) glp[0] = tau * su + 1.0;
   return lp;
 }
 
 // Constrained output row (extract() order: params, transformed params, lp__).
-template <int NCH>
+template <int NCH, int SEG = WAVE>
 __device__ void write_draw(const NutsArgs& A, const ShardDev& sh, int shard, int col, const double (&q)[NCH],
                            double lp, int lane) {
   double* out = A.draws + (size_t)shard * A.Pmax * A.S_total;
   const int D = sh.D;
   const size_t S = (size_t)A.S_total;
   if (A.family == STK_SCHOOLS) {
-    const double mu = lane_d(q[0], 0);
-    const double tau = exp(lane_d(q[0], 1));
+    const double mu = seg_bcast<SEG>(q[0], 0);
+    const double tau = exp(seg_bcast<SEG>(q[0], 1));
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
-      const int e = k * WAVE + lane;
+      const int e = k * SEG + lane;
       if (e < D) out[(size_t)e * S + col] = (e == 1) ? tau : q[k];
       if (e >= 2 && e < D) out[(size_t)(D + e - 2) * S + col] = mu + tau * q[k];
     }
   } else {
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
-      const int e = k * WAVE + lane;
+      const int e = k * SEG + lane;
       if (e < D) out[(size_t)e * S + col] = (A.family == STK_LINREG && e == D - 1) ? exp(q[k]) : q[k];
     }
   }
@@ -123,7 +149,9 @@ __device__ void write_draw(const NutsArgs& A, const ShardDev& sh, int shard, int
 }
 
 // ------------------------------------------------------------------ the chain
-template <int NCH>
+// SEG: lanes per chain (64: one chain per wave; 16 / 32: 4 / 2 chains packed in a wave, each
+// in its own DPP row(s), D <= SEG).  `lane` is the lane's position inside its segment.
+template <int NCH, int SEG = WAVE>
 struct NutsChain {
   const NutsArgs& A;
   const int gid, lane, shard, cidx, D;
@@ -148,19 +176,19 @@ struct NutsChain {
         stk(stk_),
         stks(a.stks + (size_t)gid_ * a.max_depth * SS_COUNT) {}
 
-  __device__ __forceinline__ bool ok(int k) const { return k * WAVE + lane < D; }
+  __device__ __forceinline__ bool ok(int k) const { return k * SEG + lane < D; }
   __device__ __forceinline__ double* vp(int v) const { return vec + (size_t)v * A.Dp; }
   __device__ __forceinline__ double* svp(int level, int v) const {
     return stk + ((size_t)level * SV_COUNT + v) * A.Dp;
   }
   __device__ void ld(const double* base, double (&r)[NCH]) const {
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) r[k] = ok(k) ? base[k * WAVE + lane] : 0.0;
+    for (int k = 0; k < NCH; ++k) r[k] = ok(k) ? base[k * SEG + lane] : 0.0;
   }
   __device__ void st(double* base, const double (&r)[NCH]) const {
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
-      if (ok(k)) base[k * WAVE + lane] = r[k];
+      if (ok(k)) base[k * SEG + lane] = r[k];
   }
 
   __device__ void load() {
@@ -192,15 +220,15 @@ struct NutsChain {
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
       if (ok(k)) t += pp[k] * im[k] * pp[k];
-    return 0.5 * wave_sum(t);
+    return 0.5 * seg_sum<SEG>(t);
   }
   __device__ bool criterion(const double (&psm)[NCH], const double (&psp)[NCH], const double (&rho)[NCH]) const {
     double a = 0.0, b = 0.0;
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
       if (ok(k)) { a += psp[k] * rho[k]; b += psm[k] * rho[k]; }
-    a = wave_sum(a);
-    b = wave_sum(b);
+    a = seg_sum<SEG>(a);
+    b = seg_sum<SEG>(b);
     return a > 0 && b > 0;
   }
   __device__ double uniform() {
@@ -210,7 +238,7 @@ struct NutsChain {
   __device__ void sample_momentum(uint32_t c1, uint32_t c2hi, uint32_t tag) {
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
-      const int e = k * WAVE + lane;
+      const int e = k * SEG + lane;
       p[k] = ok(k) ? normal_at(A.seed, rid, c1, c2hi, (uint32_t)e, tag) / sqrt(im[k]) : 0.0;
     }
   }
@@ -376,7 +404,7 @@ struct NutsChain {
       const int col = cidx * A.num_samples + (it - A.num_warmup);
       double qs[NCH];
       ld(vp(V_QS), qs);
-      write_draw<NCH>(A, sh, shard, col, qs, -s[S_VS], lane);
+      write_draw<NCH, SEG>(A, sh, shard, col, qs, -s[S_VS], lane);
       if (lane < N_STATS) {
         double v = 0;
         switch (lane) {
@@ -639,47 +667,70 @@ __global__ __launch_bounds__(64) void k_nuts_step(NutsArgs A, int step_id, int p
 // The chain's vector block and tree stack live in LDS for the whole launch (copied in and
 // out once): the state machine's per-leapfrog bookkeeping (z+/z-, sample point, rho, p#,
 // Welford sums, the pending sub-tree stack) then costs LDS instead of L2/HBM round trips.
-template <int NCH>
+// CPW chains share a wave (SEG = 64 / CPW lanes each, D <= SEG): at D = 10 (8 schools) one
+// chain per wave leaves 54 of 64 lanes idle, four per wave leave 24.  Every chain still runs
+// its own state machine; lanes of one chain always take the same branch, and the segmented
+// sums stay inside a chain's DPP row(s), so chains in other states never interfere.
+template <int NCH, int CPW>
 __global__ __launch_bounds__(64) void k_nuts_fused_schools(NutsArgs A, int pause_at, int max_steps) {
-  const int gid = blockIdx.x, lane = threadIdx.x;
-  extern __shared__ double fl[];
+  constexpr int SEG = WAVE / CPW;
+  static_assert(CPW == 1 || NCH == 1, "packed chains hold one chunk of lanes each");
+  const int seg = (int)threadIdx.x / SEG, lane = (int)threadIdx.x % SEG;
+  const int gid = blockIdx.x * CPW + seg;
+  const bool live = gid < A.nchains;
+  extern __shared__ double fl_all[];
   const size_t nv = (size_t)V_COUNT * A.Dp, ns = (size_t)A.max_depth * SV_COUNT * A.Dp;
+  double* const fl = fl_all + (size_t)seg * (nv + ns);
   double* const gvec = A.vec + (size_t)gid * nv;
   double* const gstk = A.stk + (size_t)gid * ns;
-  {
+  bool run = live;
+  if (run) {
     const int mode0 = A.iv[(size_t)gid * I_COUNT + I_MODE];
-    if (mode0 == M_DONE || mode0 == M_ERROR) return;
+    run = !(mode0 == M_DONE || mode0 == M_ERROR);
   }
-  for (size_t i = lane; i < nv; i += WAVE) fl[i] = gvec[i];
-  for (size_t i = lane; i < ns; i += WAVE) fl[nv + i] = gstk[i];
+  if (run) {
+    for (size_t i = lane; i < nv; i += SEG) fl[i] = gvec[i];
+    for (size_t i = lane; i < ns; i += SEG) fl[nv + i] = gstk[i];
+  }
   __syncthreads();
-  NutsChain<NCH> ch(A, gid, lane, fl, fl + nv);
-  ch.load();
-  const int mode = ch.iv[I_MODE];
-  bool req;
-  if (mode == M_PAUSED) {
-    if (ch.iv[I_ITER] >= pause_at) return;
-    req = ch.resume(pause_at);
-    if (req && lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += 1;
-  } else {
-    ch.ld(A.qeval + (size_t)gid * A.Dp, ch.q);   // the pending request
-    req = true;
+  if (run) {
+    NutsChain<NCH, SEG> ch(A, gid, lane, fl, fl + nv);
+    ch.load();
+    const int mode = ch.iv[I_MODE];
+    bool req = false, go = true;
+    if (mode == M_PAUSED) {
+      if (ch.iv[I_ITER] >= pause_at) {
+        go = false;
+      } else {
+        req = ch.resume(pause_at);
+        if (req && lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += 1;
+      }
+    } else {
+      ch.ld(A.qeval + (size_t)gid * A.Dp, ch.q);   // the pending request
+      req = true;
+    }
+    if (go) {
+      int steps = 0;
+      unsigned long long ngrad = 0;
+      while (req && steps < max_steps) {
+        double glp[NCH];
+        const double lp = schools_lpgrad<NCH, SEG>(ch.sh, ch.q, glp, lane, ch.D);
+        ++steps;
+        req = ch.consume(lp, glp, pause_at);
+        if (req) ++ngrad;
+      }
+      ch.save();
+      if (req) ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);
+      if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += ngrad;
+    } else {
+      run = false;                                  // paused at its target: nothing changed
+    }
   }
-  int steps = 0;
-  unsigned long long ngrad = 0;
-  while (req && steps < max_steps) {
-    double glp[NCH];
-    const double lp = schools_lpgrad<NCH>(ch.sh, ch.q, glp, lane, ch.D);
-    ++steps;
-    req = ch.consume(lp, glp, pause_at);
-    if (req) ++ngrad;
-  }
-  ch.save();
-  if (req) ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);
-  if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += ngrad;
   __syncthreads();
-  for (size_t i = lane; i < nv; i += WAVE) gvec[i] = fl[i];
-  for (size_t i = lane; i < ns; i += WAVE) gstk[i] = fl[nv + i];
+  if (run) {
+    for (size_t i = lane; i < nv; i += SEG) gvec[i] = fl[i];
+    for (size_t i = lane; i < ns; i += SEG) gstk[i] = fl[nv + i];
+  }
 }
 
 // lp / gradient of the 8-schools density at C points of one shard (parity hook).
@@ -713,18 +764,31 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
   hipLaunchKernelGGL(k_nuts_step<NCH>, dim3(A.nchains), dim3(64), 0, st, A, step_id, pause_at);
   return hipGetLastError();
 }
-template <int NCH>
+template <int NCH, int CPW>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
-  const size_t lds = sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * SV_COUNT * A.Dp);
+  const size_t lds = CPW * sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * SV_COUNT * A.Dp);
   if (lds > 64 * 1024) {
     // the attribute is per device: set it on every launch that needs it (a host call, once per
     // fused launch of up to max_steps leapfrogs) and report a failure as such
-    const hipError_t e = hipFuncSetAttribute((const void*)k_nuts_fused_schools<NCH>,
+    const hipError_t e = hipFuncSetAttribute((const void*)k_nuts_fused_schools<NCH, CPW>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_nuts_fused_schools<NCH>, dim3(A.nchains), dim3(64), lds, st, A, pause_at, max_steps);
+  hipLaunchKernelGGL((k_nuts_fused_schools<NCH, CPW>), dim3((A.nchains + CPW - 1) / CPW), dim3(64), lds, st, A,
+                     pause_at, max_steps);
   return hipGetLastError();
+}
+
+// chains per wave of the fused 8-schools kernel: 4 for D <= 16, 2 for D <= 32 (STARK_FUSED_CPW
+// overrides, for measurements)
+static int fused_cpw(int Dp) {
+  static const int forced = [] {
+    const char* e = getenv("STARK_FUSED_CPW");
+    return e ? atoi(e) : 0;
+  }();
+  int c = Dp <= 16 ? 4 : (Dp <= 32 ? 2 : 1);
+  if (forced == 1 || forced == 2 || forced == 4) c = std::min(c, forced);
+  return c;
 }
 
 int stk_nch_for(int Dmax) {
@@ -752,10 +816,14 @@ hipError_t stk_launch_nuts_step(const NutsArgs& A, int nch, int step_id, int pau
 }
 
 hipError_t stk_launch_nuts_fused(const NutsArgs& A, int nch, int pause_at, int max_steps, hipStream_t st) {
-  switch (nch) {
-    case 1: return launch_fused_t<1>(A, pause_at, max_steps, st);
-    case 2: return launch_fused_t<2>(A, pause_at, max_steps, st);
+  if (nch == 1) {
+    switch (fused_cpw(A.Dp)) {
+      case 4: return launch_fused_t<1, 4>(A, pause_at, max_steps, st);
+      case 2: return launch_fused_t<1, 2>(A, pause_at, max_steps, st);
+      default: return launch_fused_t<1, 1>(A, pause_at, max_steps, st);
+    }
   }
+  if (nch == 2) return launch_fused_t<2, 1>(A, pause_at, max_steps, st);
   return hipErrorInvalidValue;
 }
 

@@ -98,6 +98,26 @@ def test_adaptive_run_tracks_oracle(ctx, orc, nw, jitter):
     res.close()
 
 
+def test_packed_schools_chains_track_oracle(ctx, orc):
+    """The fused 8-schools kernel packs 4 chains per wave (16 lanes each, D = 10): 10 chains
+    over 3 waves (the last one partly empty), each with its own warmup, adaptation and tree
+    depths -- every chain's whole run equals the recursive Stan twin's."""
+    from stark_amd import engine
+    m = engine.Model(ctx, "schools", [{"y": orc.SCHOOLS_Y, "sigma": orc.SCHOOLS_SIGMA}])
+    om = orc.Model(orc.FAM_SCHOOLS, y=orc.SCHOOLS_Y, sigma=orc.SCHOOLS_SIGMA)
+    nw, ns, C = 30, 25, 10
+    s = m.sampler(num_warmup=nw, num_samples=ns, chains=C, seed=91, save_warmup=True)
+    s.run()
+    uq = s.unconstrained(0)
+    _, st = s.draws(0)
+    for c in range(C):
+        o = om.run_chain(num_warmup=nw, num_samples=ns, seed=91, gid=c)
+        err = np.abs(uq[c] - o["q"]).max()
+        assert err < 1e-8, (c, err)
+        np.testing.assert_array_equal(st[c * ns:(c + 1) * ns, 3], o["stats"][nw:, 3])   # n_leapfrog
+    s.close()
+
+
 # ---------------------------------------------------------------- statistics
 def test_schools_4096_chains_exact_moments(ctx, orc):
     """BASELINE config 2: 8 schools with 4096 parallel chains on one GPU."""
