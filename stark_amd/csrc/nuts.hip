@@ -671,8 +671,8 @@ __global__ __launch_bounds__(64) void k_nuts_step(NutsArgs A, int step_id, int p
 // chain per wave leaves 54 of 64 lanes idle, four per wave leave 24.  Every chain still runs
 // its own state machine; lanes of one chain always take the same branch, and the segmented
 // sums stay inside a chain's DPP row(s), so chains in other states never interfere.
-template <int NCH, int CPW>
-__global__ __launch_bounds__(64) void k_nuts_fused_schools(NutsArgs A, int pause_at, int max_steps) {
+template <int NCH, int CPW, int MINW = 1>
+__global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int pause_at, int max_steps) {
   constexpr int SEG = WAVE / CPW;
   static_assert(CPW == 1 || NCH == 1, "packed chains hold one chunk of lanes each");
   const int seg = (int)threadIdx.x / SEG, lane = (int)threadIdx.x % SEG;
@@ -764,17 +764,17 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
   hipLaunchKernelGGL(k_nuts_step<NCH>, dim3(A.nchains), dim3(64), 0, st, A, step_id, pause_at);
   return hipGetLastError();
 }
-template <int NCH, int CPW>
+template <int NCH, int CPW, int MINW = 1>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
   const size_t lds = CPW * sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * SV_COUNT * A.Dp);
   if (lds > 64 * 1024) {
     // the attribute is per device: set it on every launch that needs it (a host call, once per
     // fused launch of up to max_steps leapfrogs) and report a failure as such
-    const hipError_t e = hipFuncSetAttribute((const void*)k_nuts_fused_schools<NCH, CPW>,
+    const hipError_t e = hipFuncSetAttribute((const void*)k_nuts_fused_schools<NCH, CPW, MINW>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((k_nuts_fused_schools<NCH, CPW>), dim3((A.nchains + CPW - 1) / CPW), dim3(64), lds, st, A,
+  hipLaunchKernelGGL((k_nuts_fused_schools<NCH, CPW, MINW>), dim3((A.nchains + CPW - 1) / CPW), dim3(64), lds, st, A,
                      pause_at, max_steps);
   return hipGetLastError();
 }
@@ -816,10 +816,17 @@ hipError_t stk_launch_nuts_step(const NutsArgs& A, int nch, int step_id, int pau
 }
 
 hipError_t stk_launch_nuts_fused(const NutsArgs& A, int nch, int pause_at, int max_steps, hipStream_t st) {
+  static const int minw = [] {
+    const char* e = getenv("STARK_FUSED_MINW");     // measurements: 2 = two waves per SIMD (spills)
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
   if (nch == 1) {
-    switch (fused_cpw(A.Dp)) {
-      case 4: return launch_fused_t<1, 4>(A, pause_at, max_steps, st);
-      case 2: return launch_fused_t<1, 2>(A, pause_at, max_steps, st);
+    switch (fused_cpw(A.Dp) * 10 + minw) {
+      case 41: return launch_fused_t<1, 4>(A, pause_at, max_steps, st);
+      case 42: return launch_fused_t<1, 4, 2>(A, pause_at, max_steps, st);
+      case 21: return launch_fused_t<1, 2>(A, pause_at, max_steps, st);
+      case 22: return launch_fused_t<1, 2, 2>(A, pause_at, max_steps, st);
+      case 12: return launch_fused_t<1, 1, 2>(A, pause_at, max_steps, st);
       default: return launch_fused_t<1, 1>(A, pause_at, max_steps, st);
     }
   }
