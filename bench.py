@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--ess-draws", type=int, default=100,
                    help="post-warmup draws per chain for the ESS / accuracy phase (after the timed steps)")
     p.add_argument("--no-accuracy", action="store_true", help="skip the full-data Laplace reference")
+    p.add_argument("--nuts-criterion", choices=["stan2.19", "stan2.23"], default="stan2.19",
+                   help="stan2.19: the reference's pystan 2 NUTS; stan2.23: + the U-turn checks across "
+                        "subtree junctions (DESIGN.md section 4)")
     p.add_argument("--seed", type=int, default=20240)
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -160,7 +163,7 @@ def main():
     # cover the timed window and the fixed post-warmup draws of the ESS phase
     n_samp = W + K + ND + 1
     sampler = model.sampler(num_warmup=A, num_samples=n_samp, chains=a.chains, seed=a.seed + 1,
-                            shard_ids=shard_ids, stepsize_jitter=a.stepsize_jitter)
+                            shard_ids=shard_ids, stepsize_jitter=a.stepsize_jitter, nuts_criterion=a.nuts_criterion)
 
     def log(msg):
         if rank == 0:
@@ -372,7 +375,8 @@ def main():
         "config": {"workload": f"bayesian {a.family} regression, {a.shards} subposterior shards + consensus combine",
                    "rows": int(a.rows), "d": a.d, "shards": a.shards, "shards_per_gpu": spr,
                    "chains_per_shard": a.chains, "num_warmup": A, "post_warmup_draws_per_chain": n_post,
-                   "stepsize_jitter": a.stepsize_jitter, "parallelism": f"shard-dp{world}"},
+                   "stepsize_jitter": a.stepsize_jitter, "nuts_criterion": a.nuts_criterion,
+                   "parallelism": f"shard-dp{world}"},
         "ess_per_sec": ess_c / (t_adapt + t_sampling),
         "min_ess": ess_c,
         "ess_method": ("min over alpha, beta (lp__ excluded) of Stan 2.19's multi-chain ESS of the consensus draws "

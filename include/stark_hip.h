@@ -98,6 +98,11 @@ typedef struct {
                                 identically whichever GPU (and with whichever other shards) it runs */
   double stepsize_jitter;    /* Stan control stepsize_jitter in [0, 1]: every transition uses
                                 stepsize * (1 + jitter * U(-1, 1)) (base_hmc::sample_stepsize) */
+  int32_t nuts_criterion;    /* 0 (default): Stan 2.19.1's U-turn test across each merged subtree, as
+                                the reference's pystan 2 runs it; 1: also the two tests across the
+                                junction of the merged halves that Stan >= 2.23 adds (base_nuts
+                                build_tree / transition), which stop the trajectories that the single
+                                test lets run on near-isotropic Gaussian posteriors */
 } stk_config;
 
 typedef struct {

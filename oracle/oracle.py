@@ -68,7 +68,7 @@ def lib():
         L.orc_prior_lpgrad.restype = ctypes.c_double
         L.orc_run_chain.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u32, dp, dp, dp, dp, dp]
         L.orc_run_chain.restype = ctypes.c_long
-        L.orc_transition.argtypes = [ctypes.c_void_p, u64, u32, u32, ci, ctypes.c_double, dp, dp, dp, dp]
+        L.orc_transition.argtypes = [ctypes.c_void_p, u64, u32, u32, ci, ctypes.c_double, dp, dp, dp, dp, ci]
         L.orc_transition.restype = ctypes.c_long
         L.orc_logreg_grad_loop.argtypes = [i64, ci, dp, i32p, dp, dp, ci]
         L.orc_logreg_grad_loop.restype = ctypes.c_double
@@ -135,7 +135,8 @@ class _Cfg(ctypes.Structure):
                 ("adapt_delta", ctypes.c_double), ("gamma", ctypes.c_double), ("kappa", ctypes.c_double),
                 ("t0", ctypes.c_double), ("stepsize", ctypes.c_double), ("init_radius", ctypes.c_double),
                 ("init_buffer", ctypes.c_int), ("term_buffer", ctypes.c_int), ("window", ctypes.c_int),
-                ("adapt_engaged", ctypes.c_int), ("seed", ctypes.c_uint64), ("stepsize_jitter", ctypes.c_double)]
+                ("adapt_engaged", ctypes.c_int), ("seed", ctypes.c_uint64), ("stepsize_jitter", ctypes.c_double),
+                ("uturn_ext", ctypes.c_int)]
 
 
 class Model:
@@ -184,9 +185,11 @@ class Model:
     def run_chain(self, *, num_warmup=1000, num_samples=1000, max_depth=10, adapt_delta=0.8,
                   gamma=0.05, kappa=0.75, t0=10.0, stepsize=1.0, init_radius=2.0,
                   init_buffer=75, term_buffer=50, window=25, adapt_engaged=True, seed=1234,
-                  gid=0, init=None, stepsize_jitter=0.0):
+                  gid=0, init=None, stepsize_jitter=0.0, uturn_ext=False):
+        """uturn_ext: Stan >= 2.23's extra U-turn checks between subtrees (default: Stan 2.19)."""
         cfg = _Cfg(num_warmup, num_samples, max_depth, adapt_delta, gamma, kappa, t0, stepsize,
-                   init_radius, init_buffer, term_buffer, window, int(adapt_engaged), seed, stepsize_jitter)
+                   init_radius, init_buffer, term_buffer, window, int(adapt_engaged), seed, stepsize_jitter,
+                   int(bool(uturn_ext)))
         T = num_warmup + num_samples
         q = np.empty((T, self.D))
         lp = np.empty(T)
@@ -199,13 +202,13 @@ class Model:
             raise RuntimeError("oracle: step size left (0, 1e7]")
         return dict(q=q, lp=lp, stats=st, stepsize=fin[0], inv_metric=fin[1:], n_grad=ng)
 
-    def transition(self, q, *, seed, gid, iteration, eps, inv_metric=None, max_depth=10):
+    def transition(self, q, *, seed, gid, iteration, eps, inv_metric=None, max_depth=10, uturn_ext=False):
         q = np.array(q, np.float64, copy=True)
         im = np.ones(self.D) if inv_metric is None else np.ascontiguousarray(inv_metric, np.float64)
         lp = ctypes.c_double()
         st = np.empty(6)
         ng = lib().orc_transition(ctypes.byref(self._s), seed, gid, iteration, max_depth, eps,
-                                  _dp(im), _dp(q), ctypes.byref(lp), _dp(st))
+                                  _dp(im), _dp(q), ctypes.byref(lp), _dp(st), int(bool(uturn_ext)))
         return q, lp.value, st, ng
 
 

@@ -284,6 +284,7 @@ typedef struct {
   int init_buffer, term_buffer, window, adapt_engaged;
   uint64_t seed;
   double stepsize_jitter;
+  int uturn_ext;      /* 0: Stan 2.19 single criterion; 1: + the checks between subtrees (Stan >= 2.23) */
 } orc_cfg;
 
 typedef struct {
@@ -296,6 +297,7 @@ typedef struct {
   uint64_t seed;
   uint32_t gid, iter, uk;   /* uniform stream: (gid, iter, uk) */
   int divergent, depth;
+  int uturn_ext;
   ps_point z;
   long n_grad;
   /* dual averaging */
@@ -402,6 +404,66 @@ static int build_tree(nuts* s, int depth, ps_point* z_propose, double* psl, doub
   return ok;
 }
 
+/* Stan >= 2.23 base_nuts::build_tree: besides the U-turn test across the merged subtree,
+ * two tests across the junction of the two halves (the left half extended by the first
+ * momentum of the right one, and the right half extended by the last momentum of the left
+ * one), which catch trajectories that turn inside a doubling -- the resonance of the single
+ * criterion on near-isotropic Gaussian posteriors.  Tracks the begin / end momenta (p_beg,
+ * p_end) and p_sharp at both ends of every subtree. */
+static int build_tree_ext(nuts* s, int depth, ps_point* z_propose, double* ps_beg, double* ps_end, double* rho,
+                          double* p_beg, double* p_end, double H0, int sign, int* n_leapfrog, double* lsw,
+                          double* sum_metro) {
+  int D = s->D;
+  if (depth == 0) {
+    evolve(s, &s->z, sign * s->eps);
+    ++*n_leapfrog;
+    double h = Hfn(s, &s->z);
+    if (isnan(h)) h = INFINITY;
+    if ((h - H0) > s->max_deltaH) s->divergent = 1;
+    *lsw = log_sum_exp2(*lsw, H0 - h);
+    if (H0 - h > 0) *sum_metro += 1; else *sum_metro += exp(H0 - h);
+    s->z.H = h;
+    pt_copy(z_propose, &s->z, D);
+    dtau_dp(s, &s->z, ps_beg);
+    memcpy(ps_end, ps_beg, sizeof(double) * D);
+    for (int i = 0; i < D; ++i) rho[i] += s->z.p[i];
+    memcpy(p_beg, s->z.p, sizeof(double) * D);
+    memcpy(p_end, s->z.p, sizeof(double) * D);
+    return !s->divergent;
+  }
+  double* p_init_end = dalloc(D); double* ps_init_end = dalloc(D); double* rho_init = dalloc(D);
+  double* p_final_beg = dalloc(D); double* ps_final_beg = dalloc(D); double* rho_final = dalloc(D);
+  double* ext = dalloc(D);
+  double lsw_init = -INFINITY, lsw_final = -INFINITY;
+  int ok = build_tree_ext(s, depth - 1, z_propose, ps_beg, ps_init_end, rho_init, p_beg, p_init_end, H0, sign,
+                          n_leapfrog, &lsw_init, sum_metro);
+  if (ok) {
+    ps_point zr; pt_alloc(&zr, D); pt_copy(&zr, &s->z, D);
+    ok = build_tree_ext(s, depth - 1, &zr, ps_final_beg, ps_end, rho_final, p_final_beg, p_end, H0, sign,
+                        n_leapfrog, &lsw_final, sum_metro);
+    if (ok) {
+      double lsw_sub = log_sum_exp2(lsw_init, lsw_final);
+      *lsw = log_sum_exp2(*lsw, lsw_sub);
+      double u = rand_uniform(s);   /* consumed unconditionally (RNG spec) */
+      if (lsw_final > lsw_sub) pt_copy(z_propose, &zr, D);
+      else if (u < exp(lsw_final - lsw_sub)) pt_copy(z_propose, &zr, D);
+      double* rho_sub = dalloc(D);
+      for (int i = 0; i < D; ++i) { rho_sub[i] = rho_init[i] + rho_final[i]; rho[i] += rho_sub[i]; }
+      int c1 = compute_criterion(D, ps_beg, ps_end, rho_sub);
+      for (int i = 0; i < D; ++i) ext[i] = rho_init[i] + p_final_beg[i];
+      int c2 = compute_criterion(D, ps_beg, ps_final_beg, ext);
+      for (int i = 0; i < D; ++i) ext[i] = rho_final[i] + p_init_end[i];
+      int c3 = compute_criterion(D, ps_init_end, ps_end, ext);
+      ok = c1 && c2 && c3;
+      free(rho_sub);
+    }
+    pt_free(&zr);
+  }
+  free(p_init_end); free(ps_init_end); free(rho_init); free(p_final_beg); free(ps_final_beg); free(rho_final);
+  free(ext);
+  return ok;
+}
+
 typedef struct { double accept, eps, depth, n_leapfrog, divergent, energy; } orc_stats;
 
 /* base_nuts::transition (Stan 2.19.1).  s->z holds the start point with V and g valid. */
@@ -425,7 +487,48 @@ static void transition(nuts* s, orc_stats* st) {
   double lsw = 0.0;
   int n_leapfrog = 0; double sum_metro = 0.0;
   s->depth = 0; s->divergent = 0;
-  while (s->depth < s->max_depth) {
+  /* Stan >= 2.23 bookkeeping: momenta / p_sharp at both ends of the backward and forward parts */
+  double* p_ff = dalloc(D); double* p_fb = dalloc(D); double* p_bf = dalloc(D); double* p_bb = dalloc(D);
+  double* ps_fb = dalloc(D); double* ps_bf = dalloc(D); double* rho_f = dalloc(D); double* rho_b = dalloc(D);
+  double* ext = dalloc(D);
+  memcpy(p_ff, s->z.p, sizeof(double) * D); memcpy(p_fb, p_ff, sizeof(double) * D);
+  memcpy(p_bf, p_ff, sizeof(double) * D); memcpy(p_bb, p_ff, sizeof(double) * D);
+  memcpy(ps_fb, psp, sizeof(double) * D); memcpy(ps_bf, psp, sizeof(double) * D);
+  while (s->uturn_ext && s->depth < s->max_depth) {
+    int valid;
+    double lsw_sub = -INFINITY;
+    memset(rho_f, 0, sizeof(double) * D); memset(rho_b, 0, sizeof(double) * D);
+    if (rand_uniform(s) > 0.5) {
+      memcpy(rho_b, rho, sizeof(double) * D);
+      memcpy(p_bf, p_ff, sizeof(double) * D); memcpy(ps_bf, psp, sizeof(double) * D);
+      pt_copy(&s->z, &z_plus, D);
+      valid = build_tree_ext(s, s->depth, &z_propose, ps_fb, psp, rho_f, p_fb, p_ff, H0, 1, &n_leapfrog, &lsw_sub,
+                             &sum_metro);
+      pt_copy(&z_plus, &s->z, D);
+    } else {
+      memcpy(rho_f, rho, sizeof(double) * D);
+      memcpy(p_fb, p_bb, sizeof(double) * D); memcpy(ps_fb, psm, sizeof(double) * D);
+      pt_copy(&s->z, &z_minus, D);
+      valid = build_tree_ext(s, s->depth, &z_propose, ps_bf, psm, rho_b, p_bf, p_bb, H0, -1, &n_leapfrog, &lsw_sub,
+                             &sum_metro);
+      pt_copy(&z_minus, &s->z, D);
+    }
+    if (!valid) break;
+    ++s->depth;
+    double u = rand_uniform(s);     /* consumed unconditionally (RNG spec) */
+    if (lsw_sub > lsw) pt_copy(&z_sample, &z_propose, D);
+    else if (u < exp(lsw_sub - lsw)) pt_copy(&z_sample, &z_propose, D);
+    lsw = log_sum_exp2(lsw, lsw_sub);
+    for (int i = 0; i < D; ++i) rho[i] = rho_b[i] + rho_f[i];
+    int c1 = compute_criterion(D, psm, psp, rho);
+    for (int i = 0; i < D; ++i) ext[i] = rho_b[i] + p_fb[i];
+    int c2 = compute_criterion(D, psm, ps_fb, ext);
+    for (int i = 0; i < D; ++i) ext[i] = rho_f[i] + p_bf[i];
+    int c3 = compute_criterion(D, ps_bf, psp, ext);
+    if (!(c1 && c2 && c3)) break;
+  }
+  free(p_ff); free(p_fb); free(p_bf); free(p_bb); free(ps_fb); free(ps_bf); free(rho_f); free(rho_b); free(ext);
+  while (!s->uturn_ext && s->depth < s->max_depth) {
     memset(rho_sub, 0, sizeof(double) * D);
     int valid;
     double lsw_sub = -INFINITY;
@@ -591,6 +694,7 @@ long orc_run_chain(const orc_data* m, const orc_cfg* cfg, uint32_t gid, const do
   update_potential_gradient(&s, &s.z);
   s.nom_eps = cfg->stepsize;
   s.jitter = cfg->stepsize_jitter;
+  s.uturn_ext = cfg->uturn_ext;
   s.delta = cfg->adapt_delta; s.gamma = cfg->gamma; s.kappa = cfg->kappa; s.t0 = cfg->t0;
   s.mu = log(10.0 * cfg->stepsize);
   da_restart(&s);
@@ -628,9 +732,10 @@ long orc_run_chain(const orc_data* m, const orc_cfg* cfg, uint32_t gid, const do
 /* One fixed-step-size transition from (q, inv_metric, eps) with no adaptation: the unit
  * the GPU/CPU trajectory-parity test compares.  Writes the new q, lp, stats. */
 long orc_transition(const orc_data* m, uint64_t seed, uint32_t gid, uint32_t iter, int max_depth,
-                    double eps, const double* inv_metric, double* q, double* lp, double* st_out) {
+                    double eps, const double* inv_metric, double* q, double* lp, double* st_out, int uturn_ext) {
   nuts s; memset(&s, 0, sizeof(s));
   s.m = m; s.D = orc_dim(m); s.seed = seed; s.gid = gid; s.iter = iter;
+  s.uturn_ext = uturn_ext;
   int D = s.D;
   s.inv_metric = dalloc(D); memcpy(s.inv_metric, inv_metric, sizeof(double) * D);
   s.max_depth = max_depth; s.max_deltaH = 1000.0; s.nom_eps = eps;

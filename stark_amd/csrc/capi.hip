@@ -521,6 +521,7 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   ARG_CHECK(cfg->adapt_delta > 0 && cfg->adapt_delta < 1, "adapt_delta must be in (0, 1)");
   ARG_CHECK(cfg->stepsize > 0, "stepsize must be positive");
   ARG_CHECK(cfg->stepsize_jitter >= 0 && cfg->stepsize_jitter <= 1, "stepsize_jitter must be in [0, 1]");
+  ARG_CHECK(cfg->nuts_criterion == 0 || cfg->nuts_criterion == 1, "nuts_criterion must be 0 (Stan 2.19) or 1 (Stan >= 2.23)");
   stk_ctx* ctx = m->ctx;
   STK_HIP_CHECK(hipSetDevice(ctx->device));
   const int nch = stk_nch_for(m->Dmax);
@@ -562,6 +563,7 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   A.t0 = cfg->adapt_t0;
   A.seed = cfg->seed;
   A.jitter = cfg->stepsize_jitter;
+  A.uturn_ext = cfg->nuts_criterion;
   A.S_total = cfg->chains * cfg->num_samples;
   A.Pmax = m->Pmax;
   A.shards = m->sh_dev.as<ShardDev>();

@@ -58,7 +58,9 @@ enum Vec : int {
   V_WM, V_WM2,          // Welford mean / M2
   V_COUNT
 };
-enum StackVec : int { SV_RHO, SV_PSB, SV_Q, SV_G, SV_COUNT };   // pending left subtree per level
+// pending left subtree per level; SV_PB / SV_PE / SV_PSE (its first / last momentum and last
+// p_sharp) serve the Stan >= 2.23 checks across subtree junctions (nuts_criterion = 1)
+enum StackVec : int { SV_RHO, SV_PSB, SV_Q, SV_G, SV_PB, SV_PE, SV_PSE, SV_COUNT };
 enum Scal : int {
   S_V, S_VF, S_VB, S_VS, S_HS, S_H0, S_LSW, S_EPS, S_NOMEPS, S_SUMMETRO,
   S_DA_CNT, S_SBAR, S_XBAR, S_MU, S_WFN, S_PH0, S_LFEPS, S_COUNT
@@ -98,6 +100,7 @@ struct NutsArgs {
   int* req_step;    // nshards: last step index that issued a request for the shard
   const int* shard_ids;  // nullptr or global shard index per local shard (RNG stream keys)
   double jitter;         // stepsize_jitter (0: off)
+  int uturn_ext;         // nuts_criterion: 1 = Stan >= 2.23 extra U-turn checks
 };
 
 // RNG stream of a chain: global shard index * chains + chain.

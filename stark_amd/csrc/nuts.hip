@@ -487,7 +487,7 @@ struct NutsChain {
     s[S_SUMMETRO] += (H0 - h > 0) ? 1.0 : exp(H0 - h);
     // the leaf as a depth-0 sub-tree
     double c_lsw = H0 - h;
-    double c_rho[NCH], c_psb[NCH], c_pse[NCH], c_q[NCH], c_g[NCH];
+    double c_rho[NCH], c_psb[NCH], c_pse[NCH], c_q[NCH], c_g[NCH], c_pb[NCH];
     double c_V = s[S_V], c_H = h;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
@@ -496,6 +496,7 @@ struct NutsChain {
       c_pse[k] = c_psb[k];
       c_q[k] = q[k];
       c_g[k] = g[k];
+      c_pb[k] = p[k];
     }
     if (iv[I_DIV]) return end_transition(pause_at);
     const int depth = iv[I_DEPTH];
@@ -516,13 +517,32 @@ struct NutsChain {
         c_V = stks[j * SS_COUNT + SS_V];
         c_H = stks[j * SS_COUNT + SS_H];
       }
+      bool junction_ok = true;
+      if (A.uturn_ext) {
+        // Stan >= 2.23: the left half extended by the right half's first momentum, and the
+        // right half extended by the left half's last momentum, must not turn either
+        double l_pb[NCH], l_pe[NCH], l_pse[NCH], e1[NCH], e2[NCH];
+        ld(svp(j, SV_PB), l_pb);
+        ld(svp(j, SV_PE), l_pe);
+        ld(svp(j, SV_PSE), l_pse);
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+          e1[k] = l_rho[k] + c_pb[k];
+          e2[k] = c_rho[k] + l_pe[k];
+          c_pb[k] = l_pb[k];
+        }
+        const bool ok2 = criterion(l_psb, c_psb, e1);
+        const bool ok3 = criterion(l_pse, c_pse, e2);
+        junction_ok = ok2 && ok3;
+      }
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
         c_rho[k] = l_rho[k] + c_rho[k];
         c_psb[k] = l_psb[k];
       }
       c_lsw = lsw_sub;
-      if (!criterion(l_psb, c_pse, c_rho)) return end_transition(pause_at);
+      const bool ok1 = criterion(l_psb, c_pse, c_rho);
+      if (!ok1 || !junction_ok) return end_transition(pause_at);
       ++j;
     }
     if (j < depth) {
@@ -531,6 +551,11 @@ struct NutsChain {
       st(svp(j, SV_PSB), c_psb);
       st(svp(j, SV_Q), c_q);
       st(svp(j, SV_G), c_g);
+      if (A.uturn_ext) {
+        st(svp(j, SV_PB), c_pb);
+        st(svp(j, SV_PE), p);          // its last leaf is the latest one
+        st(svp(j, SV_PSE), c_pse);
+      }
       stks[j * SS_COUNT + SS_LSW] = c_lsw;
       stks[j * SS_COUNT + SS_V] = c_V;
       stks[j * SS_COUNT + SS_H] = c_H;
@@ -540,6 +565,11 @@ struct NutsChain {
     }
     // the top-level sub-tree of this depth is complete and valid
     const int fwd = iv[I_DIR] > 0;
+    double o_p[NCH], o_ps[NCH];     // the old trajectory's end next to the new sub-tree
+    if (A.uturn_ext) {
+      ld(vp(fwd ? V_PF : V_PB), o_p);
+      ld(vp(fwd ? V_PSP : V_PSM), o_ps);
+    }
     st(vp(fwd ? V_QF : V_QB), q);
     st(vp(fwd ? V_PF : V_PB), p);
     st(vp(fwd ? V_GF : V_GB), g);
@@ -553,10 +583,13 @@ struct NutsChain {
       s[S_HS] = c_H;
     }
     s[S_LSW] = log_sum_exp2(s[S_LSW], c_lsw);
-    double rho[NCH], psp[NCH], psm[NCH];
+    double rho[NCH], psp[NCH], psm[NCH], rho_old[NCH];
     ld(vp(V_RHO), rho);
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) rho[k] = rho[k] + c_rho[k];
+    for (int k = 0; k < NCH; ++k) {
+      rho_old[k] = rho[k];
+      rho[k] = rho[k] + c_rho[k];
+    }
     st(vp(V_RHO), rho);
     if (fwd) {
       st(vp(V_PSP), c_pse);
@@ -569,6 +602,20 @@ struct NutsChain {
       for (int k = 0; k < NCH; ++k) psm[k] = c_pse[k];
       ld(vp(V_PSP), psp);
     }
+    bool junction_ok = true;
+    if (A.uturn_ext) {
+      // the new sub-tree against the old trajectory across their junction (base_nuts::transition)
+      double e1[NCH], e2[NCH];
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        e1[k] = fwd ? rho_old[k] + c_pb[k] : c_rho[k] + o_p[k];
+        e2[k] = fwd ? c_rho[k] + o_p[k] : rho_old[k] + c_pb[k];
+      }
+      const bool ok2 = fwd ? criterion(psm, c_psb, e1) : criterion(c_pse, o_ps, e1);
+      const bool ok3 = fwd ? criterion(o_ps, c_pse, e2) : criterion(c_psb, psp, e2);
+      junction_ok = ok2 && ok3;
+    }
+    if (!junction_ok) return end_transition(pause_at);
     if (!criterion(psm, psp, rho) || iv[I_DEPTH] >= A.max_depth) return end_transition(pause_at);
     begin_subtree();
     return true;

@@ -120,13 +120,19 @@ def make_config(num_warmup=1000, num_samples=1000, chains=1, max_depth=10, adapt
                 adapt_kappa=0.75, adapt_t0=10.0, stepsize=1.0, init_radius=2.0, adapt_init_buffer=75,
                 adapt_term_buffer=50, adapt_window=25, adapt_engaged=True, seed=1234, init=None,
                 inv_metric=None, skip_init_stepsize=False, iter_offset=0, shard_ids=None,
-                save_warmup=False, stepsize_jitter=0.0):
-    """Stan sampler settings (pystan 2 `sampling()` keywords + control block)."""
+                save_warmup=False, stepsize_jitter=0.0, nuts_criterion="stan2.19"):
+    """Stan sampler settings (pystan 2 `sampling()` keywords + control block).
+    nuts_criterion: "stan2.19" (the reference's pystan 2: one U-turn test per merged subtree)
+    or "stan2.23" (plus the checks across subtree junctions of Stan >= 2.23)."""
     c = _lib.default_config()
     c.num_warmup, c.num_samples, c.chains, c.max_depth = int(num_warmup), int(num_samples), int(chains), int(max_depth)
     c.adapt_delta, c.adapt_gamma, c.adapt_kappa, c.adapt_t0 = adapt_delta, adapt_gamma, adapt_kappa, adapt_t0
     c.stepsize, c.init_radius = stepsize, init_radius
     c.stepsize_jitter = float(stepsize_jitter)
+    crit = {"stan2.19": 0, "stan2.23": 1, 0: 0, 1: 1}
+    if nuts_criterion not in crit:
+        raise ValueError(f"nuts_criterion must be 'stan2.19' or 'stan2.23', got {nuts_criterion!r}")
+    c.nuts_criterion = crit[nuts_criterion]
     c.adapt_init_buffer, c.adapt_term_buffer, c.adapt_window = adapt_init_buffer, adapt_term_buffer, adapt_window
     c.adapt_engaged = int(bool(adapt_engaged))
     c.seed = int(seed) & 0xFFFFFFFFFFFFFFFF

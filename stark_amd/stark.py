@@ -96,7 +96,7 @@ _CONTROL_KEYS = {"adapt_delta": "adapt_delta", "max_treedepth": "max_depth", "st
                  "adapt_gamma": "adapt_gamma", "adapt_kappa": "adapt_kappa", "adapt_t0": "adapt_t0",
                  "adapt_init_buffer": "adapt_init_buffer", "adapt_term_buffer": "adapt_term_buffer",
                  "adapt_window": "adapt_window", "adapt_engaged": "adapt_engaged", "inv_metric": "inv_metric",
-                 "stepsize_jitter": "stepsize_jitter"}
+                 "stepsize_jitter": "stepsize_jitter", "nuts_criterion": "nuts_criterion"}
 
 
 def _unconstrain(family, data, init_dict):

@@ -377,3 +377,91 @@ def test_fulldata_two_ranks_share_one_gpu():
         assert p.exitcode == 0
     assert all(r[1] and r[2] for r in res)
     assert res[0][3] == res[1][3] > 0
+
+
+# ---------------------------------------------------------------- Stan >= 2.23 U-turn checks (nuts_criterion)
+@pytest.mark.parametrize("jitter", [0.0, 0.5])
+def test_extended_criterion_tracks_oracle(ctx, orc, jitter):
+    """nuts_criterion='stan2.23' (the checks across subtree junctions, at every merge and at
+    the top level) against the recursive twin with the same checks: a whole adaptive run."""
+    from stark_amd import engine
+    rng = np.random.default_rng(31)
+    n, d = 500, 3
+    X = rng.uniform(-1.7, 1.7, (n, d))
+    y = (rng.uniform(size=n) < 1 / (1 + np.exp(-(0.3 + X @ np.array([0.8, -0.4, 0.2]))))).astype(np.int32)
+    m = engine.Model(ctx, "logistic", [{"x": X, "y": y}])
+    om = orc.Model(orc.FAM_LOGREG, X=X, y=y)
+    nw, ns, C = 30, 30, 3
+    s = m.sampler(num_warmup=nw, num_samples=ns, chains=C, seed=77, save_warmup=True, stepsize_jitter=jitter,
+                  nuts_criterion="stan2.23")
+    s.run()
+    uq = s.unconstrained(0)
+    _, st = s.draws(0)
+    for c in range(C):
+        o = om.run_chain(num_warmup=nw, num_samples=ns, seed=77, gid=c, stepsize_jitter=jitter, uturn_ext=True)
+        err = np.abs(uq[c] - o["q"]).max()
+        assert err < 1e-8, (c, err)
+        np.testing.assert_array_equal(st[c * ns:(c + 1) * ns, 3], o["stats"][nw:, 3])
+    s.close()
+
+
+def test_extended_criterion_schools_packed(ctx, orc):
+    """The same checks in the fused 8-schools kernel (4 chains per wave): every chain starts
+    on the recursive twin's path."""
+    from stark_amd import engine
+    m = engine.Model(ctx, "schools", [{"y": orc.SCHOOLS_Y, "sigma": orc.SCHOOLS_SIGMA}])
+    om = orc.Model(orc.FAM_SCHOOLS, y=orc.SCHOOLS_Y, sigma=orc.SCHOOLS_SIGMA)
+    s = m.sampler(num_warmup=30, num_samples=20, chains=6, seed=5, save_warmup=True, nuts_criterion="stan2.23")
+    s.run()
+    uq = s.unconstrained(0)
+    for c in range(6):
+        o = om.run_chain(num_warmup=30, num_samples=20, seed=5, gid=c, uturn_ext=True)
+        err = np.abs(uq[c] - o["q"]).max(axis=1)
+        assert err[:10].max() < 1e-8, (c, err[:10])
+    s.close()
+    m.close()
+
+
+def test_extended_criterion_stops_resonant_trajectories(ctx):
+    """On a near-isotropic Gaussian posterior (logistic regression, 2e4 rows, d = 100, unit
+    metric scaled to the posterior sd) at a step size where 8 leapfrogs span half an orbit,
+    Stan 2.19's single test lets trajectories run (depth 5-9); the junction checks stop them."""
+    from stark_amd import engine
+    m = engine.Model.synthetic(ctx, "logistic", 1, 20000, 100, data_seed=5)
+    beta = engine.Model.gen_beta(5, 100)
+    sd = 1 / np.sqrt(20000 * 0.2)
+    init = np.concatenate([[0.0], beta])
+    lf = {}
+    for crit in ("stan2.19", "stan2.23"):
+        s = m.sampler(num_warmup=0, num_samples=40, chains=16, seed=3, stepsize=0.40, skip_init_stepsize=True,
+                      adapt_engaged=False, inv_metric=np.full(101, sd * sd), init=np.tile(init, 16),
+                      nuts_criterion=crit)
+        s.run()
+        lf[crit] = s.draws(0)[1][:, 3].mean()
+        s.close()
+    assert lf["stan2.19"] > 2.5 * lf["stan2.23"], lf
+    assert lf["stan2.23"] < 20, lf
+    m.close()
+
+
+@pytest.mark.parametrize("C", [4, 16])
+def test_extended_criterion_moments(ctx, orc, C):
+    """Statistical check of the extended criterion: logistic moments vs the 2.19 twin."""
+    from stark_amd import engine
+    rng = np.random.default_rng(12)
+    n, d = 3000, 4
+    X = rng.uniform(-1.7, 1.7, (n, d))
+    y = (rng.uniform(size=n) < 1 / (1 + np.exp(-(0.2 + X @ rng.normal(0, 0.6, d))))).astype(np.int32)
+    m = engine.Model(ctx, "logistic", [{"x": X, "y": y}])
+    s = m.sampler(num_warmup=500, num_samples=1000, chains=C, seed=8, nuts_criterion="stan2.23")
+    s.run()
+    g = s.unconstrained(0)
+    om = orc.Model(orc.FAM_LOGREG, X=X, y=y)
+    runs = [om.run_chain(num_warmup=500, num_samples=1000, seed=99, gid=c) for c in range(4)]
+    o = np.stack([r["q"][500:] for r in runs])
+    for k in range(d + 1):
+        a, b = g[:, :, k], o[:, :, k]
+        se = np.hypot(a.std() / np.sqrt(ess(a)), b.std() / np.sqrt(ess(b)))
+        assert abs(a.mean() - b.mean()) < 5 * se, (k, a.mean(), b.mean(), se)
+        assert abs(a.std() / b.std() - 1) < 0.1
+    s.close()
