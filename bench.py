@@ -262,6 +262,27 @@ def main():
         lap = L.laplace(model, list(range(spr)), pooled.mean(1), pooled.std(1) / np.sqrt(a.shards),
                         reduce=(lambda arr: allreduce(arr)) if dist else None)
         log(f"full-data Laplace reference in {time.perf_counter() - t:.1f}s")
+    lin = None
+    if a.family == "linear" and not a.no_accuracy:
+        # flat-prior linear regression: the full-data posterior of (alpha, beta) in closed form
+        # (multivariate t) from the sufficient statistics [1 X]'[1 X], [1 X]'y, y'y, summed
+        # over every shard of every rank
+        k = a.d + 1
+        acc = np.zeros(k * k + k + 2)
+        for s_ in range(spr):
+            dd = model.copy_data(s_)
+            A1 = np.hstack([np.ones((dd["x"].shape[0], 1)), dd["x"]])
+            acc[:k * k] += (A1.T @ A1).ravel()
+            acc[k * k:k * k + k] += A1.T @ dd["y"]
+            acc[-2] += dd["y"] @ dd["y"]
+            acc[-1] += dd["x"].shape[0]
+            del A1, dd
+        allreduce(acc)
+        AtA, Aty, yty, ntot = acc[:k * k].reshape(k, k), acc[k * k:k * k + k], acc[-2], acc[-1]
+        mean = np.linalg.solve(AtA, Aty)
+        rss = yty - 2 * mean @ Aty + mean @ AtA @ mean
+        nu = ntot - k - 1
+        lin = (mean, nu / (nu - 2.0) * rss / nu * np.linalg.inv(AtA))
     sampler.close()
 
     if rank != 0:
@@ -304,6 +325,16 @@ def main():
             "sd_ratio_median": float(np.median(csd / fsd)),
             "truth": zz(truth - fm, fsd),
             "newton_steps_in_sd": finfo["newton_steps_in_sd"]}
+    if lin is not None:
+        fm, fc = lin
+        fsd = np.sqrt(np.diag(fc))
+        k = a.d + 1
+        accuracy["vs_fulldata_exact"] = {
+            "consensus": zz(comb[:k].mean(1) - fm, fsd),
+            "consensus_joint_lp": zz(comb_joint[:k].mean(1) - fm, fsd),
+            "sd_ratio_median": float(np.median(comb[:k].std(1) / fsd)),
+            "truth": zz(truth[:k] - fm, fsd),
+            "note": "alpha, beta vs the closed-form flat-prior posterior (multivariate t) of all N rows"}
     accuracy["note"] = ("z = (mean - reference) / reference sd per parameter over all alpha, beta; the consensus "
                         "puts lp__ in its own weight block (engine.consensus separate_lp); *_joint_lp = the "
                         "reference's joint combine (lp__ inside inv(cov), stark/stark.py:49-56). vs_fulldata_laplace: "

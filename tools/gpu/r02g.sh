@@ -9,3 +9,5 @@ rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ] || exit 3
 timeout -k 10 120 python3 tools/combine_bench.py > $O/r02g_combine.json 2>&1 || exit 6
 timeout -k 10 560 python3 bench.py --steps 20 --warmup 5 --nuts-criterion stan2.23 > $O/r02g_bench_223.json 2> $O/r02g_bench_223.err
 echo "bench rc=$?"
+timeout -k 10 400 python3 bench.py --family linear --rows 1e7 --d 50 --adapt-iters 1000 --steps 200 --warmup 5 --ess-draws 200 --no-cpu-baseline > $O/r02g_bench_linear.json 2> $O/r02g_bench_linear.err
+echo "linear rc=$?"
