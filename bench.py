@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--nuts-criterion", choices=["stan2.19", "stan2.23"], default="stan2.19",
                    help="stan2.19: the reference's pystan 2 NUTS; stan2.23: + the U-turn checks across "
                         "subtree junctions (DESIGN.md section 4)")
+    p.add_argument("--second-criterion", choices=["stan2.23", "stan2.19", "none"], default="stan2.23",
+                   help="after the main run: a second adaptation + ESS phase on the same data with this "
+                        "NUTS criterion, reported as ess_second_criterion")
     p.add_argument("--seed", type=int, default=20240)
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -262,6 +265,32 @@ def main():
         lap = L.laplace(model, list(range(spr)), pooled.mean(1), pooled.std(1) / np.sqrt(a.shards),
                         reduce=(lambda arr: allreduce(arr)) if dist else None)
         log(f"full-data Laplace reference in {time.perf_counter() - t:.1f}s")
+    second = None
+    if a.second_criterion != "none" and a.second_criterion != a.nuts_criterion:
+        # the same data, warmup length and post-warmup draws, another U-turn criterion
+        t = time.perf_counter()
+        s2 = model.sampler(num_warmup=A, num_samples=ND, chains=a.chains, seed=a.seed + 1, shard_ids=shard_ids,
+                           stepsize_jitter=a.stepsize_jitter, nuts_criterion=a.second_criterion)
+        s2.run(A)
+        ctx.sync()
+        barrier()
+        t2_adapt = time.perf_counter() - t
+        t = time.perf_counter()
+        s2.run(A + ND)
+        ctx.sync()
+        barrier()
+        t2_post = time.perf_counter() - t
+        loc2, st2 = {}, []
+        for s_ in range(spr):
+            dr, st = s2.draws(s_)
+            loc2[shard_ids[s_]] = np.ascontiguousarray(dr)
+            st2.append(st)
+        allp2 = sdist.all_gather_partitions(loc2, a.shards)
+        st2 = np.vstack(st2)
+        second = {"allp": allp2, "t_adapt": t2_adapt, "t_post": t2_post,
+                  "lf": float(st2[:, 3].mean()), "div": s2.info()["divergent"]}
+        s2.close()
+        log(f"second criterion {a.second_criterion}: adaptation {t2_adapt:.1f}s, {ND} draws {t2_post:.1f}s")
     lin = None
     if a.family == "linear" and not a.no_accuracy:
         # flat-prior linear regression: the full-data posterior of (alpha, beta) in closed form
@@ -294,6 +323,7 @@ def main():
 
     from stark_amd import diagnostics
     P = allp[0].shape[0]
+    engine.consensus(allp, ctx, separate_lp=True)            # first call sizes the scratch buffers
     t = time.perf_counter()
     comb, used = engine.consensus(allp, ctx, separate_lp=True)
     t_comb = time.perf_counter() - t
@@ -335,6 +365,20 @@ def main():
             "sd_ratio_median": float(np.median(comb[:k].std(1) / fsd)),
             "truth": zz(truth[:k] - fm, fsd),
             "note": "alpha, beta vs the closed-form flat-prior posterior (multivariate t) of all N rows"}
+    if second is not None:
+        comb2, _ = engine.consensus(second["allp"], ctx, separate_lp=True)
+        ess2 = float(np.nanmin([diagnostics.ess(comb2[p].reshape(C, ND)) for p in range(comb2.shape[0] - 1)]))
+        second_line = {"nuts_criterion": a.second_criterion, "ess_per_sec": ess2 / (second["t_adapt"] + second["t_post"]),
+                       "min_ess": ess2, "ess_per_sec_post_warmup": ess2 / second["t_post"],
+                       "leapfrogs_per_transition": second["lf"], "divergent": second["div"],
+                       "seconds": {"adaptation": second["t_adapt"], "post_warmup_draws": second["t_post"]}}
+        if lap is not None:
+            second_line["vs_fulldata_laplace"] = zz(comb2[:-1].mean(1) - lap[0], np.sqrt(np.diag(lap[1])))
+        if lin is not None:
+            k = a.d + 1
+            second_line["vs_fulldata_exact"] = zz(comb2[:k].mean(1) - lin[0], np.sqrt(np.diag(lin[1])))
+    else:
+        second_line = None
     accuracy["note"] = ("z = (mean - reference) / reference sd per parameter over all alpha, beta; the consensus "
                         "puts lp__ in its own weight block (engine.consensus separate_lp); *_joint_lp = the "
                         "reference's joint combine (lp__ inside inv(cov), stark/stark.py:49-56). vs_fulldata_laplace: "
@@ -418,6 +462,7 @@ def main():
         "num_warmup_note": (f"num_warmup = {A} (Stan's default iter=2000 would warm up for 1000; DESIGN.md 4): "
                             "the adaptation is the dominant ESS/s cost"),
         "subposterior_min_ess_shard0": ess_s0,
+        "ess_second_criterion": second_line,
         "accuracy": accuracy,
         "stepsize_per_chain": {"min": float(eps.min()), "median": float(np.median(eps)), "max": float(eps.max())},
         "treedepth_mean": float(stats[:, 2].mean()),

@@ -391,7 +391,7 @@ def test_extended_criterion_tracks_oracle(ctx, orc, jitter):
     y = (rng.uniform(size=n) < 1 / (1 + np.exp(-(0.3 + X @ np.array([0.8, -0.4, 0.2]))))).astype(np.int32)
     m = engine.Model(ctx, "logistic", [{"x": X, "y": y}])
     om = orc.Model(orc.FAM_LOGREG, X=X, y=y)
-    nw, ns, C = 30, 30, 3
+    nw, ns, C = 30, 30, 4
     s = m.sampler(num_warmup=nw, num_samples=ns, chains=C, seed=77, save_warmup=True, stepsize_jitter=jitter,
                   nuts_criterion="stan2.23")
     s.run()

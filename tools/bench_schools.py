@@ -5,9 +5,16 @@ The data are example/stark_ex.py:4-6 (J = 8, embedded here: /root/reference does
 the GPU box); the program is example/schools.stan (non-centred: mu, tau, eta[J]).  All 4096
 chains run Stan's defaults (1000 warmup with adaptation + 1000 draws) in the fused kernel
 (k_nuts_fused_schools: one wave per chain, the O(J) gradient inline, up to 4096 leapfrogs per
-launch).  Reported: chain-gradient evaluations per second over the whole run and over the
-sampling phase, and ESS/s of the sampling phase (min over mu, tau, eta, theta of Stan 2.19's
-multi-chain ESS over all 4096 chains).
+launch; 4 chains share a wave at J = 8, 16 lanes each).  Reported: chain-gradient evaluations
+per second over the whole run and over the sampling phase, ESS/s of the sampling phase (min
+over mu, tau, eta, theta of Stan 2.19's multi-chain ESS over all 4096 chains), and a VALU
+roofline line: the gradient's fp64 operations (FLOPS_PER_GRAD, counted from schools_lpgrad
+in nuts.hip: 14 per school -- theta = mu + tau eta (2), z = (y - theta) / sigma (2), r = z /
+sigma (1), lp += -eta^2/2 - z^2/2 (4), the three sums (3), grad eta (2) -- plus exp(tau),
+the Jacobian and the two sum finishes) times gradients/s, against the 78.6 TF fp64 peak.
+The NUTS bookkeeping around each gradient (kinetic energy, U-turn dot products, multinomial
+log-sum-exp, Philox) is not counted: it is what bounds this kernel -- a serial chain of
+dependent fp64 operations per leapfrog, latency-bound at one wave per SIMD.
 """
 import json
 import os
@@ -19,6 +26,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+FLOPS_PER_GRAD = lambda J: 14 * J + 4
+FP64_PEAK_TFS = 78.6
 Y = [28.0, 8.0, -3.0, 7.0, -1.0, 1.0, 18.0, 12.0]        # example/stark_ex.py:5
 SIGMA = [15.0, 10.0, 16.0, 11.0, 9.0, 11.0, 10.0, 18.0]  # example/stark_ex.py:6
 
@@ -62,7 +71,13 @@ def main():
         "leapfrogs_per_transition": (i2["leapfrogs"] - i1["leapfrogs"]) / (a.chains * a.samples),
         "divergent": i2["divergent"], "accept_stat_mean": float(stats[:, 0].mean()),
         "posterior_mean_mu_tau": [float(draws[0].mean()), float(draws[1].mean())],
+        "roofline": {"bound": "fp64 VALU (latency-bound state machine)",
+                     "achieved": (i2["grad_evals"] - i1["grad_evals"]) / samp * FLOPS_PER_GRAD(len(Y)) / 1e12,
+                     "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                     "flops_per_grad": FLOPS_PER_GRAD(len(Y))},
+        "chains_per_wave": int(os.environ.get("STARK_FUSED_CPW", "4")),
     }
+    line["roofline"]["frac"] = line["roofline"]["achieved"] / FP64_PEAK_TFS
     print(json.dumps(line), flush=True)
     s.close()
     m.close()

@@ -115,6 +115,7 @@ def main():
     p.add_argument("--block", type=int, default=50)
     p.add_argument("--seed", type=int, default=20240)
     p.add_argument("--jitter", type=float, default=0.5)
+    p.add_argument("--nuts-criterion", choices=["stan2.19", "stan2.23"], default="stan2.19")
     p.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "consensus_check.jsonl"))
     a = p.parse_args()
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
@@ -122,7 +123,7 @@ def main():
     rps = int(a.rows) // a.shards
     m = engine.Model.synthetic(ctx, "logistic", a.shards, rps, a.d, data_seed=a.seed)
     s = m.sampler(num_warmup=a.warmup, num_samples=a.samples, chains=a.chains, seed=a.seed + 1,
-                  stepsize_jitter=a.jitter)
+                  stepsize_jitter=a.jitter, nuts_criterion=a.nuts_criterion)
     truth = np.concatenate([[0.0], engine.Model.gen_beta(a.seed, a.d)])
     t0 = time.perf_counter()
     log = lambda msg: print(f"[consensus_check {time.perf_counter() - t0:7.1f}s] {msg}", file=sys.stderr, flush=True)
