@@ -49,6 +49,66 @@ __global__ __launch_bounds__(256) void k_mfma(const double* src, double* sink, u
   }
 }
 
+// fp64 VALU FMA rate: NACC independent v_fma_f64 chains per lane (operands in VGPRs), and
+// the same with one operand a wave-uniform SGPR value (the beta-from-scalar-registers form).
+template <int NACC, bool SOP>
+__global__ __launch_bounds__(256) void k_fma(const double* src, double* sink, unsigned long long* stamps, int iters) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  double b = src[(t * 7 + 13) & 4095];
+  if (SOP) b = __builtin_amdgcn_readfirstlane((int)t) == 12345 ? 1.0 : src[blockIdx.x & 4095];
+  double acc[NACC];
+  double a[NACC];
+#pragma unroll
+  for (int j = 0; j < NACC; ++j) { acc[j] = src[(t + j) & 4095]; a[j] = src[(t + 3 * j + 1) & 4095]; }
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < NACC; ++j) acc[j] = fma(a[j], b, acc[j]);
+  }
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < NACC; ++j) s += acc[j];
+  if (s == 12345.678) sink[t] = s;
+  if (threadIdx.x == 0) {
+    stamps[2 * blockIdx.x] = c1 - c0;
+    stamps[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
+template <int NACC, bool SOP>
+static void run_fma(int wps, int iters, const double* src, double* sink, unsigned long long* st, int ncu) {
+  const int nb = ncu * wps;
+  hipLaunchKernelGGL((k_fma<NACC, SOP>), dim3(nb), dim3(256), 0, 0, src, sink, st, iters);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float best = 1e30f;
+  for (int r = 0; r < 5; ++r) {
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL((k_fma<NACC, SOP>), dim3(nb), dim3(256), 0, 0, src, sink, st, iters);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    best = std::min(best, ms);
+  }
+  std::vector<unsigned long long> h(2 * nb);
+  CK(hipMemcpy(h.data(), st, sizeof(unsigned long long) * 2 * nb, hipMemcpyDeviceToHost));
+  std::vector<double> clk(nb);
+  for (int b = 0; b < nb; ++b) clk[b] = (double)h[2 * b] / (double)h[2 * b + 1] * 100.0;
+  std::sort(clk.begin(), clk.end());
+  const double flops = (double)nb * 256 * iters * NACC * 2.0;
+  const double instr_per_simd = (double)wps * iters * NACC;
+  const double cyc = clk[nb / 2] * 1e6 * best * 1e-3 / instr_per_simd;
+  printf("v_fma_f64 %s  waves/SIMD %d  chains %2d  %8.3f ms  %6.1f TF/s  clock %6.0f MHz  cycles/instr/SIMD %5.2f\n",
+         SOP ? "sgpr-op" : "vgpr   ", wps, NACC, best, flops / best / 1e9, clk[nb / 2], cyc);
+  fflush(stdout);
+}
+
 template <int NACC>
 static void run(int wps, int iters, const double* src, double* sink, unsigned long long* st, int ncu) {
   const int nb = ncu * 4 * wps / 4;   // 256-thread blocks: 4 waves each, one per SIMD
@@ -100,5 +160,10 @@ int main(int argc, char** argv) {
     run<8>(w, iters, src, sink, st, ncu);
   }
   run<16>(1, iters, src, sink, st, ncu);
+  for (int w : {1, 2, 4}) {
+    run_fma<8, false>(w, iters * 4, src, sink, st, ncu);
+    run_fma<16, false>(w, iters * 2, src, sink, st, ncu);
+    run_fma<8, true>(w, iters * 4, src, sink, st, ncu);
+  }
   return 0;
 }
