@@ -186,34 +186,32 @@ __global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t*
 }
 
 // In-place Gauss-Jordan inverse of a batch of SPD P x P matrices (P <= 128), the matrix held
-// in REGISTERS: 256 threads = 128 columns x 2 row halves, thread (j, g) owns A[64 g + r][j],
-// r < 64 (one wave per SIMD, 128 VGPRs of matrix).  Step k needs row k and column k as they
-// stood after step k-1; the threads owning elements of row / column k+1 publish them into
-// the other half of a double-buffered LDS pair while they update, so each step costs one
-// barrier.  The rank-1 update is one FMA per element (column-k entries read as broadcasts,
-// two per ds_read_b128); row k is the wave-uniform register a[k - 64 g]; column k is one
-// lane's fix-up.  Padding to 128 x 128 with an identity block keeps every element in range.
-// Shard b with used[b] == 0 (NaN draws) gets W = 0 and no status; status[b] = 1 when a pivot
-// is <= 0 or NaN (singular covariance: numpy's inv raises LinAlgError).
-constexpr int SI_R = 64;
-__global__ __launch_bounds__(256) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
-                                                     int32_t* status) {
-  __shared__ __attribute__((aligned(16))) double rowk[2][128];
-  __shared__ __attribute__((aligned(16))) double colk[2][128];
+// in REGISTERS: 1024 threads = 128 columns x 8 row groups, thread (j, g) owns A[g + 8 r][j],
+// r < 16.  Step k needs row k and column k as they stood after step k-1; the threads owning
+// elements of row / column k+1 publish them into the other half of a double-buffered LDS
+// pair while they update, so each step costs one barrier.  Shard b with used[b] == 0 (NaN
+// draws) gets W = 0 and no status; status[b] = 1 when a pivot is <= 0 or NaN (singular
+// covariance: numpy's inv raises LinAlgError).
+constexpr int SI_R = 16;
+__global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
+                                                      int32_t* status) {
+  __shared__ double rowk[2][128];
+  __shared__ double colk[2][128];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int j = tid & 127, g = uniform_int(tid >> 7);   // g: wave-uniform row half
-  const int i0 = 64 * g;
+  const int j = tid & 127, g = uniform_int(tid >> 7);   // g: wave-uniform row group
   const double* M = Min + (size_t)b * P * P;
   double* out = Out + (size_t)b * P * P;
   if (used && !used[b]) {
-    for (int i = tid; i < P * P; i += 256) out[i] = 0.0;
+    for (int i = tid; i < P * P; i += 1024) out[i] = 0.0;
     if (tid == 0) status[b] = 0;
     return;
   }
+  // padded to 128 x 128 with an identity block: padding rows/columns have zero coupling, so
+  // the P pivot steps leave them untouched and no element needs a bounds test in the loop
   double a[SI_R];
 #pragma unroll
   for (int r = 0; r < SI_R; ++r) {
-    const int i = i0 + r;
+    const int i = g + 8 * r;
     a[r] = (i < P && j < P) ? M[(size_t)i * P + j] : (i == j ? 1.0 : 0.0);
     if (i == 0) rowk[0][j] = a[r];
     if (j == 0) colk[0][i] = a[r];
@@ -228,38 +226,30 @@ __global__ __launch_bounds__(256) void k_spd_inverse(const double* Min, double* 
     ip = fma(ip, fma(-piv, ip, 1.0), ip);
     ip = fma(ip, fma(-piv, ip, 1.0), ip);
     const double rj = rowk[cur][j] * ip;
-    const dbl2* cc = reinterpret_cast<const dbl2*>(&colk[cur][i0]);
+    double ci[SI_R];
 #pragma unroll
-    for (int r = 0; r < SI_R; r += 2) {
-      const dbl2 c2 = cc[r >> 1];
-      a[r] = fma(-c2.x, rj, a[r]);
-      a[r + 1] = fma(-c2.y, rj, a[r + 1]);
+    for (int r = 0; r < SI_R; ++r) ci[r] = colk[cur][g + 8 * r];   // broadcast reads
+#pragma unroll
+    for (int r = 0; r < SI_R; ++r) a[r] = fma(-ci[r], rj, a[r]);   // the rank-1 update: 1 FMA per element
+    if (j == k) {                                                  // column k: one lane
+#pragma unroll
+      for (int r = 0; r < SI_R; ++r) a[r] = -ci[r] * ip;
     }
-    if (j == k) {                               // column k: one lane
 #pragma unroll
-      for (int r = 0; r < SI_R; r += 2) {
-        const dbl2 c2 = cc[r >> 1];
-        a[r] = -c2.x * ip;
-        a[r + 1] = -c2.y * ip;
-      }
-    }
-    const int rk = k - i0;                      // wave-uniform: scalar compares, no register indexing
-    if (rk >= -1 && rk < SI_R) {
-#pragma unroll
-      for (int r = 0; r < SI_R; ++r) {
-        if (r == rk) a[r] = (j == k) ? ip : rj;
-        if (r == rk + 1) rowk[nxt][j] = a[r];
-      }
+    for (int r = 0; r < SI_R; ++r) {
+      const int i = g + 8 * r;                                     // wave-uniform tests
+      if (i == k) a[r] = (j == k) ? ip : rj;
+      if (i == k + 1) rowk[nxt][j] = a[r];
     }
     if (j == k + 1) {
 #pragma unroll
-      for (int r = 0; r < SI_R; ++r) colk[nxt][i0 + r] = a[r];
+      for (int r = 0; r < SI_R; ++r) colk[nxt][g + 8 * r] = a[r];
     }
     __syncthreads();
   }
 #pragma unroll
   for (int r = 0; r < SI_R; ++r) {
-    const int i = i0 + r;
+    const int i = g + 8 * r;
     if (i < P && j < P) out[(size_t)i * P + j] = a[r];
   }
   if (tid == 0) status[b] = sing;
@@ -378,7 +368,7 @@ static bool lds_inverse_fits(int P) { return P <= 128; }
 hipError_t stk_launch_spd_inverse(const double* M, double* Inv, double* work, int P, int batch, const int32_t* used,
                                   int32_t* status, hipStream_t st) {
   if (lds_inverse_fits(P)) {
-    hipLaunchKernelGGL(k_spd_inverse, dim3(batch), dim3(256), 0, st, M, Inv, P, used, status);
+    hipLaunchKernelGGL(k_spd_inverse, dim3(batch), dim3(1024), 0, st, M, Inv, P, used, status);
   } else {
     hipLaunchKernelGGL(k_gj_inverse, dim3(batch), dim3(1024), 0, st, M, work, Inv, P, used, status);
   }
