@@ -34,6 +34,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_PEAK_TFS = 78.6    # MI355X fp64 matrix (= vector) spec, dense
+FP64_MFMA_MEASURED_TFS = 47.9   # v_mfma_f64_16x16x4 back to back, 4 waves/SIMD, clock-stamped at 2.38 GHz
+                                # (tools/mfma_ceiling.hip, profiles/r02b_mfma_ceiling.log)
 
 
 def parse():
@@ -418,7 +420,8 @@ def main():
                 "frac": (tfs / FP64_PEAK_TFS) if tfs else None, "traffic": traffic,
                 "kernel": f"{kname}<{fam}> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
                 "algorithmic_flops_per_launch": flops_per_launch, "algorithmic_bytes_per_launch": bytes_per_launch,
-                "hbm": hbm}
+                "peak_measured": FP64_MFMA_MEASURED_TFS,
+                "frac_of_measured": (tfs / FP64_MFMA_MEASURED_TFS) if tfs else None, "hbm": hbm}
     else:
         roof = dict(bound="hbm", **{k: v for k, v in hbm.items()}, traffic=traffic,
                     kernel=f"k_sweep3<{fam},{a.chains}>", avg_launch_ms=avg_ms,
