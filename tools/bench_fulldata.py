@@ -39,6 +39,7 @@ def main():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--seed", type=int, default=20240)
     p.add_argument("--init-radius", type=float, default=2.0, help="pystan init_r (Stan default 2)")
+    p.add_argument("--nuts-criterion", choices=["stan2.19", "stan2.23"], default="stan2.19")
     p.add_argument("--adapt-iters", type=int, default=0,
                    help="> 0: run Stan's warmup (untimed) first and report ESS/s of the transitions the "
                         "chains complete inside the timed window")
@@ -71,7 +72,8 @@ def main():
     nw = A if A > 0 else 1000
     total = nw + K + W + 1
     fs = fulldata.FullDataSampler(model, num_warmup=nw, num_samples=total - nw, chains=a.chains, seed=a.seed + 1,
-                                  stepsize_jitter=0.5 if A > 0 else 0.0, init_radius=a.init_radius)
+                                  stepsize_jitter=0.5 if A > 0 else 0.0, init_radius=a.init_radius,
+                                  nuts_criterion=a.nuts_criterion)
     if rank == 0:
         print(f"[bench_fulldata] {world} GPU(s) x {rows} rows x d={a.d}: {model.device_bytes() / 1e9:.1f} GB/GPU, "
               f"generated in {t_gen:.1f}s", file=sys.stderr, flush=True)
@@ -142,13 +144,15 @@ def main():
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (Philox in HBM, SURVEY 8d)",
         "config": {"workload": "full-data HMC/NUTS logistic regression, per-leapfrog gradient all-reduce",
                    "rows_total": rows * world, "rows_per_gpu": rows, "d": a.d, "chains": a.chains,
-                   "parallelism": f"row-dp{world}", "note": "N=1e9 (8 TB) exceeds node HBM; rows per GPU resident"},
+                   "parallelism": f"row-dp{world}", "nuts_criterion": a.nuts_criterion,
+                   "note": "N=1e9 (8 TB) exceeds node HBM; rows per GPU resident"},
         "rows_x_chains_per_sec": grads * rows * world / elapsed,
         "ess_per_sec": ess_ps, "min_ess": min_ess, "adapt_iters": A,
         "transitions_in_window": ({"min": int((it1 - it0).min()), "median": float(np.median(it1 - it0))}
                                   if A > 0 else None),
         "roofline": {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": tfs / FP64_PEAK_TFS, "traffic": None,
+                     "frac": tfs / FP64_PEAK_TFS, "traffic": None, "peak_measured": 47.9,
+                     "frac_of_measured": tfs / 47.9,
                      "kernel": "k_gemm_fwd + k_gemm_bwd (fp64 MFMA 16x16x4, 64 chains)", "avg_launch_ms": avg_ms,
                      "algorithmic_flops_per_launch": flops,
                      "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
