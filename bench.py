@@ -141,7 +141,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
-    if world > 1:
+    # STARK_FORCE_DIST=1: a process group even at world size 1 (exercises the RCCL collectives of
+    # the N-rank path on one GPU: all-reduces, the draw all-gather, the Laplace gradient sums)
+    if world > 1 or os.environ.get("STARK_FORCE_DIST") == "1":
         import torch.distributed as dist
         local_rank %= torch.cuda.device_count()
         torch.cuda.set_device(local_rank)
