@@ -187,3 +187,27 @@ def test_consensus_avg_reduce_skips_nan_in_any_position(ctx, orc):
     sep, used = engine.consensus([f[0], f[1], bad], ctx, separate_lp=True)
     assert list(used) == [True, True, False]
     np.testing.assert_allclose(sep[:-1], orc.consensus_combine_ref([x[:-1] for x in f[:2]]), rtol=1e-9, atol=1e-11)
+
+
+def test_extract_permuted_order_through_the_driver(ctx):
+    """Stark draws come back in pystan's extract(permuted=True) order: the chain-order run
+    (permuted=False) with permute_draws applied, for the same seed, column for column."""
+    import os
+    from stark_amd import stark
+    from stark_amd.rdd import LocalContext
+    sc = LocalContext()
+    school = list(zip([28, 8, -3, 7, -1, 1, 18, 12], [15, 10, 16, 11, 9, 11, 10, 18]))
+
+    def prep(data):
+        return {"J": len(data), "y": [d[0] for d in data], "sigma": [d[1] for d in data]}
+
+    st = stark.Stark(sc, sc.parallelize(school, 2), prep)
+    st.setStanModel(file=os.path.join(os.path.dirname(os.path.dirname(__file__)), "stark_amd", "models",
+                                      "schools.stan"))
+    datas = [prep(p) for p in sc.parallelize(school, 2).partitions()]
+    kw = dict(iter=300, chains=2, seed=17)
+    perm = st._sample_partitions(datas, shard_ids=[0, 1], **kw)
+    plain = st._sample_partitions(datas, shard_ids=[0, 1], permuted=False, **kw)
+    for p in range(2):
+        np.testing.assert_array_equal(perm[p], stark.permute_draws(plain[p], 2, 17, p))
+        assert not np.array_equal(perm[p], plain[p])
