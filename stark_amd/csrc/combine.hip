@@ -32,7 +32,6 @@
 namespace stk {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
-struct __attribute__((aligned(16))) double4_t { double x, y, z, w; };
 constexpr int CB_T = 64;     // output tile
 constexpr int CB_K = 16;     // K slice
 
@@ -186,26 +185,18 @@ __global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t*
   used[s] = bad ? 0 : 1;
 }
 
-// In-place BLOCK Gauss-Jordan inverse of a batch of SPD P x P matrices (P <= 128), the matrix
-// held in REGISTERS: 1024 threads = 128 columns x 8 row groups, thread (j, g) owns
-// A[g + 8 r][j], r < 16.  Pivots go four at a time (block K = {k .. k+3}, B = A_KK):
-//   A_KK <- B^-1,  A_Kj <- B^-1 A_Kj,  A_iK <- -A_iK B^-1,  A_ij <- A_ij - A_iK B^-1 A_Kj,
-// the exact-arithmetic equivalent of four single pivots, so 26 barriers at P = 102 instead of
-// 102.  B^-1 (4 x 4, SPD) is formed by every thread from the published rows; each thread
-// forms r(j) = B^-1 A_Kj for its column (16 FMAs) and updates each of its elements with 4 FMAs
-// (A_iK read as LDS broadcasts).  Rows / columns of the next block are published into the
-// other half of a double-buffered LDS pair while they are updated.  The matrix is padded to
-// 128 x 128 with an identity block (zero coupling: the padding never changes), so P need not
-// be a multiple of 4.  A diagonal pivot <= 0 or NaN inside B's factorisation marks the matrix
-// singular (numpy's inv raises LinAlgError); shard b with used[b] == 0 gets W = 0.
+// In-place Gauss-Jordan inverse of a batch of SPD P x P matrices (P <= 128), the matrix held
+// in REGISTERS: 1024 threads = 128 columns x 8 row groups, thread (j, g) owns A[g + 8 r][j],
+// r < 16.  Step k needs row k and column k as they stood after step k-1; the threads owning
+// elements of row / column k+1 publish them into the other half of a double-buffered LDS
+// pair while they update, so each step costs one barrier.  Shard b with used[b] == 0 (NaN
+// draws) gets W = 0 and no status; status[b] = 1 when a pivot is <= 0 or NaN (singular
+// covariance: numpy's inv raises LinAlgError).
 constexpr int SI_R = 16;
-__device__ __forceinline__ double sel4(double x0, double x1, double x2, double x3, int i) {
-  return i == 0 ? x0 : (i == 1 ? x1 : (i == 2 ? x2 : x3));
-}
 __global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
                                                       int32_t* status) {
-  __shared__ __attribute__((aligned(16))) double rowsK[2][4][128];
-  __shared__ __attribute__((aligned(16))) double colsK[2][128][4];
+  __shared__ double rowk[2][128];
+  __shared__ double colk[2][128];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int j = tid & 127, g = uniform_int(tid >> 7);   // g: wave-uniform row group
   const double* M = Min + (size_t)b * P * P;
@@ -215,83 +206,44 @@ __global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double*
     if (tid == 0) status[b] = 0;
     return;
   }
+  // padded to 128 x 128 with an identity block: padding rows/columns have zero coupling, so
+  // the P pivot steps leave them untouched and no element needs a bounds test in the loop
   double a[SI_R];
 #pragma unroll
   for (int r = 0; r < SI_R; ++r) {
     const int i = g + 8 * r;
     a[r] = (i < P && j < P) ? M[(size_t)i * P + j] : (i == j ? 1.0 : 0.0);
-    if (i < 4) rowsK[0][i][j] = a[r];
-    if (j < 4) colsK[0][i][j] = a[r];
+    if (i == 0) rowk[0][j] = a[r];
+    if (j == 0) colk[0][i] = a[r];
   }
   __syncthreads();
   int sing = 0;
-  const int P4 = (P + 3) & ~3;
-  for (int k = 0; k < P4; k += 4) {
-    const int cur = (k >> 2) & 1, nxt = cur ^ 1;
-    // B^-1 by single-pivot Gauss-Jordan on the 4 x 4 block (every thread, registers)
-    double Bi[4][4];
+  for (int k = 0; k < P; ++k) {
+    const int cur = k & 1, nxt = cur ^ 1;
+    const double piv = rowk[cur][k];
+    if (!(piv > 0.0)) { sing = 1; break; }      // uniform: every thread read the same pivot
+    double ip = __builtin_amdgcn_rcp(piv);      // 1/piv to the last ulp: two Newton steps
+    ip = fma(ip, fma(-piv, ip, 1.0), ip);
+    ip = fma(ip, fma(-piv, ip, 1.0), ip);
+    const double rj = rowk[cur][j] * ip;
+    double ci[SI_R];
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int r = 0; r < SI_R; ++r) ci[r] = colk[cur][g + 8 * r];   // broadcast reads
 #pragma unroll
-      for (int l = 0; l < 4; ++l) Bi[m][l] = rowsK[cur][m][k + l];
-    bool ok = true;
+    for (int r = 0; r < SI_R; ++r) a[r] = fma(-ci[r], rj, a[r]);   // the rank-1 update: 1 FMA per element
+    if (j == k) {                                                  // column k: one lane
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const double piv = Bi[q][q];
-      ok = ok && (piv > 0.0);
-      double ip = __builtin_amdgcn_rcp(piv);
-      ip = fma(ip, fma(-piv, ip, 1.0), ip);
-      ip = fma(ip, fma(-piv, ip, 1.0), ip);
-      double rq[4], cq[4];
-#pragma unroll
-      for (int l = 0; l < 4; ++l) { rq[l] = Bi[q][l] * ip; cq[l] = Bi[l][q]; }
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int l = 0; l < 4; ++l) {
-          double v = fma(-cq[m], rq[l], Bi[m][l]);
-          if (m == q) v = (l == q) ? ip : rq[l];
-          else if (l == q) v = -cq[m] * ip;
-          Bi[m][l] = v;
-        }
-    }
-    if (!ok) { sing = 1; break; }               // uniform: every thread formed the same B^-1
-    // r(j) = B^-1 A_Kj for this thread's column
-    double rj[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      double v = 0.0;
-#pragma unroll
-      for (int l = 0; l < 4; ++l) v = fma(Bi[m][l], rowsK[cur][l][j], v);
-      rj[m] = v;
-    }
-    const bool jK = j >= k && j < k + 4;
-    const int mj = j - k;                       // this lane's index inside the block (jK)
-    // the values a pivot-block row takes in this column (no register indexing: selects)
-    double rowv[4], bcol[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      rowv[m] = jK ? sel4(Bi[m][0], Bi[m][1], Bi[m][2], Bi[m][3], mj) : rj[m];
-      bcol[m] = sel4(Bi[m][0], Bi[m][1], Bi[m][2], Bi[m][3], mj);     // B^-1[m][j - k]
+      for (int r = 0; r < SI_R; ++r) a[r] = -ci[r] * ip;
     }
 #pragma unroll
     for (int r = 0; r < SI_R; ++r) {
-      const int i = g + 8 * r;                  // wave-uniform
-      const double4_t c = *reinterpret_cast<const double4_t*>(&colsK[cur][i][0]);
-      double v;
-      if (i >= k && i < k + 4) {                // row of the pivot block: B^-1 A_Kj (or B^-1)
-        v = sel4(rowv[0], rowv[1], rowv[2], rowv[3], i - k);
-      } else if (jK) {                          // column of the pivot block: -A_iK B^-1
-        v = -(c.x * bcol[0] + c.y * bcol[1] + c.z * bcol[2] + c.w * bcol[3]);
-      } else {
-        v = fma(-c.x, rj[0], a[r]);
-        v = fma(-c.y, rj[1], v);
-        v = fma(-c.z, rj[2], v);
-        v = fma(-c.w, rj[3], v);
-      }
-      a[r] = v;
-      if (i >= k + 4 && i < k + 8) rowsK[nxt][i - k - 4][j] = v;
-      if (j >= k + 4 && j < k + 8) colsK[nxt][i][j - k - 4] = v;
+      const int i = g + 8 * r;                                     // wave-uniform tests
+      if (i == k) a[r] = (j == k) ? ip : rj;
+      if (i == k + 1) rowk[nxt][j] = a[r];
+    }
+    if (j == k + 1) {
+#pragma unroll
+      for (int r = 0; r < SI_R; ++r) colk[nxt][g + 8 * r] = a[r];
     }
     __syncthreads();
   }
