@@ -35,7 +35,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_PEAK_TFS = 78.6    # MI355X fp64 matrix (= vector) spec, dense
 FP64_MFMA_MEASURED_TFS = 47.9   # v_mfma_f64_16x16x4 back to back, 4 waves/SIMD, clock-stamped at 2.38 GHz
-                                # (tools/mfma_ceiling.hip, profiles/r02b_mfma_ceiling.log)
+                                # (tools/mfma_ceiling.hip, profiles/r02b_mfma_ceiling.log): the instruction the sweep issues
+FP64_MFMA4_MEASURED_TFS = 75.2  # v_mfma_f64_4x4x4_4b back to back (profiles/r02n_mfma4.log): the chip's fp64 ceiling;
+                                # the sweep cannot feed it ("the four-block form")
 
 
 def parse():
@@ -423,7 +425,9 @@ def main():
                 "kernel": f"{kname}<{fam}> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
                 "algorithmic_flops_per_launch": flops_per_launch, "algorithmic_bytes_per_launch": bytes_per_launch,
                 "peak_measured": FP64_MFMA_MEASURED_TFS,
-                "frac_of_measured": (tfs / FP64_MFMA_MEASURED_TFS) if tfs else None, "hbm": hbm}
+                "peak_measured_instruction": "v_mfma_f64_16x16x4_f64 (the kernel's)",
+                "frac_of_measured": (tfs / FP64_MFMA_MEASURED_TFS) if tfs else None,
+                "peak_measured_4x4x4_4b": FP64_MFMA4_MEASURED_TFS, "hbm": hbm}
     else:
         roof = dict(bound="hbm", **{k: v for k, v in hbm.items()}, traffic=traffic,
                     kernel=f"k_sweep3<{fam},{a.chains}>", avg_launch_ms=avg_ms,

@@ -38,7 +38,7 @@ def test_schools_lpgrad(ctx, orc):
                                    # v4 fp64 MFMA (16 chains per launch; 20 = two batches, the second padded)
                                    (1, 1, 16), (7, 3, 16), (1000, 100, 16), (4097, 50, 16), (333, 128, 16),
                                    (65, 104, 20), (20000, 100, 16), (64, 65, 16), (5000, 2, 16), (129, 17, 16),
-                                   (333, 129, 16),
+                                   (333, 129, 16), (3, 100, 16), (9, 50, 16), (100003, 100, 16),
                                    # v5 two-pass fp64 MFMA GEMMs (64 chains; 70 = two batches)
                                    (1, 1, 64), (7, 3, 64), (4097, 50, 64), (333, 129, 64), (257, 300, 64),
                                    (1000, 1000, 64), (130, 1001, 70), (5000, 100, 64)])

@@ -288,6 +288,35 @@ int main(int argc, char** argv) {
     abl("v4 -bwd", k_sweepm<STK_LOGREG, 25, 7, 2, SM_MINB, true>);
     abl("v4 -fwd", k_sweepm<STK_LOGREG, 25, 7, 4, SM_MINB, true>);
     abl("v4 -all", k_sweepm<STK_LOGREG, 25, 7, 7, SM_MINB, true>);
+    {   // k_sweepq (4x4x4 four-block MFMA), S = 8, NB = 3, two blocks per CU: ablations
+      const size_t lq = sweepq_lds(8, 3, 25, d);
+      auto kq = [&](const char* name, auto kern) {
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        timeit(name, bytes, [&] { hipLaunchKernelGGL(kern, dim3(nsh * G), dim3(256), lq, st, A4); });
+      };
+      kq("q", k_sweepq<STK_LOGREG, 25, 8, 3, 2, 0>);
+      kq("q -trans", k_sweepq<STK_LOGREG, 25, 8, 3, 2, 1>);
+      kq("q -bwd", k_sweepq<STK_LOGREG, 25, 8, 3, 2, 2>);
+      kq("q -fwd", k_sweepq<STK_LOGREG, 25, 8, 3, 2, 4>);
+      kq("q -all", k_sweepq<STK_LOGREG, 25, 8, 3, 2, 7>);
+      kq("q -lds", k_sweepq<STK_LOGREG, 25, 8, 3, 2, 8>);
+      kq("q -lds-trans", k_sweepq<STK_LOGREG, 25, 8, 3, 2, 9>);
+      kq("q4 -lds-trans", k_sweepq<STK_LOGREG, 25, 4, 6, 2, 9>);
+    }
+    {   // k_sweepx (4x4x4, rotated row groups, two register images per sub-tile)
+      const size_t lx = sweepx_lds(25, d);
+      auto kx = [&](const char* name, auto kern) {
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        timeit(name, bytes, [&] { hipLaunchKernelGGL(kern, dim3(nsh * G), dim3(256), lx, st, A4); });
+      };
+      kx("x", k_sweepx<STK_LOGREG, 25, 2, 0>);
+      kx("x -trans", k_sweepx<STK_LOGREG, 25, 2, 1>);
+      kx("x -bwd", k_sweepx<STK_LOGREG, 25, 2, 2>);
+      kx("x -fwd", k_sweepx<STK_LOGREG, 25, 2, 4>);
+      kx("x -all", k_sweepx<STK_LOGREG, 25, 2, 7>);
+      kx("x -lds", k_sweepx<STK_LOGREG, 25, 2, 8>);
+      kx("x 1blk", k_sweepx<STK_LOGREG, 25, 1, 0>);
+    }
     const double fl = 4.0 * d * C * (double)rows * nsh;   // algorithmic fp64 flops of one sweep
     timeit("v4 flops", fl, [&] {
       CK(stk_launch_sweep(STK_LOGREG, sh_d, 0, nsh, rows, d, T, LD, G, G, lds, q, C, Dp, partial, nullptr, 0, nullptr, st, wsp));
