@@ -7,6 +7,17 @@
 
 namespace stk {
 
+typedef __attribute__((address_space(3))) void* lds_vptr;
+// Buffer descriptor built from readfirstlane'd inputs, so the compiler can prove it
+// wave-uniform and keeps it in SGPRs (no waterfall loop around every buffer op).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int64_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
+}
+
 constexpr int WAVE = 64;
 
 // Pointers fetched from device structs are generic to the compiler: loads through them

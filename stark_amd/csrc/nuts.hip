@@ -30,6 +30,7 @@
 
 namespace stk {
 
+
 // Lane exchange of a double by DPP (VALU, a few cycles; __shfl is a ds_bpermute round trip).
 template <int CTRL>
 __device__ __forceinline__ double nuts_dpp(double v) {
@@ -124,7 +125,7 @@ __device__ double schools_lpgrad(const ShardDev& sh, const double (&q)[NCH], dou
 
 // Constrained output row (extract() order: params, transformed params, lp__).
 template <int NCH, int SEG = WAVE>
-__device__ void write_draw(const NutsArgs& A, const ShardDev& sh, int shard, int col, const double (&q)[NCH],
+__device__ __forceinline__ void write_draw(const NutsArgs& A, const ShardDev& sh, int shard, int col, const double (&q)[NCH],
                            double lp, int lane) {
   double* out = A.draws + (size_t)shard * A.Pmax * A.S_total;
   const int D = sh.D;
@@ -152,6 +153,9 @@ __device__ void write_draw(const NutsArgs& A, const ShardDev& sh, int shard, int
 // SEG: lanes per chain (64: one chain per wave; 16 / 32: 4 / 2 chains packed in a wave, each
 // in its own DPP row(s), D <= SEG).  `lane` is the lane's position inside its segment.
 template <int NCH, int SEG = WAVE>
+// (every member is force-inlined: a non-inlined constructor or method receiving `this` puts
+// the whole chain object -- s[], iv[], q, p, g -- in scratch memory; 48.7 -> 26.1 us per step,
+// profiles/r02q_kernel_stats.csv vs r02r_kernel_stats_global.csv)
 struct NutsChain {
   const NutsArgs& A;
   const int gid, lane, shard, cidx, D;
@@ -164,11 +168,11 @@ struct NutsChain {
   int iv[I_COUNT];
   double q[NCH], p[NCH], g[NCH], im[NCH];
 
-  __device__ NutsChain(const NutsArgs& a, int gid_, int lane_)
+  __device__ __forceinline__ NutsChain(const NutsArgs& a, int gid_, int lane_)
       : NutsChain(a, gid_, lane_, a.vec + (size_t)gid_ * V_COUNT * a.Dp,
                   a.stk + (size_t)gid_ * a.max_depth * SV_COUNT * a.Dp) {}
   // vec_ / stk_: this chain's vector block and tree stack (global memory, or an LDS copy)
-  __device__ NutsChain(const NutsArgs& a, int gid_, int lane_, double* vec_, double* stk_)
+  __device__ __forceinline__ NutsChain(const NutsArgs& a, int gid_, int lane_, double* vec_, double* stk_)
       : A(a), gid(gid_), lane(lane_), shard(gid_ / a.C), cidx(gid_ % a.C), D(a.shards[gid_ / a.C].D),
         rid(rng_stream(a, gid_)),
         sh(a.shards[gid_ / a.C]),
@@ -181,29 +185,35 @@ struct NutsChain {
   __device__ __forceinline__ double* svp(int level, int v) const {
     return stk + ((size_t)level * SV_COUNT + v) * A.Dp;
   }
-  __device__ void ld(const double* base, double (&r)[NCH]) const {
+  __device__ __forceinline__ void ld(const double* base, double (&r)[NCH]) const {
 #pragma unroll
     for (int k = 0; k < NCH; ++k) r[k] = ok(k) ? base[k * SEG + lane] : 0.0;
   }
-  __device__ void st(double* base, const double (&r)[NCH]) const {
+  __device__ __forceinline__ void st(double* base, const double (&r)[NCH]) const {
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
       if (ok(k)) base[k * SEG + lane] = r[k];
   }
 
-  __device__ void load() {
+  __device__ __forceinline__ void load() {
+    load_scalars();
+    load_vectors();
+  }
+  __device__ __forceinline__ void load_scalars() {
     const double* sc = A.sc + (size_t)gid * S_COUNT;
     const int* ivp = A.iv + (size_t)gid * I_COUNT;
 #pragma unroll
     for (int i = 0; i < S_COUNT; ++i) s[i] = sc[i];
 #pragma unroll
     for (int i = 0; i < I_COUNT; ++i) iv[i] = ivp[i];
+  }
+  __device__ __forceinline__ void load_vectors() {
     ld(vp(V_Q), q);
     ld(vp(V_P), p);
     ld(vp(V_G), g);
     ld(vp(V_IM), im);
   }
-  __device__ void save() const {
+  __device__ __forceinline__ void save() const {
     double* sc = A.sc + (size_t)gid * S_COUNT;
     int* ivp = A.iv + (size_t)gid * I_COUNT;
 #pragma unroll
@@ -215,14 +225,14 @@ struct NutsChain {
     st(vp(V_G), g);
   }
 
-  __device__ double kinetic(const double (&pp)[NCH]) const {   // diag_e_metric::tau
+  __device__ __forceinline__ double kinetic(const double (&pp)[NCH]) const {   // diag_e_metric::tau
     double t = 0.0;
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
       if (ok(k)) t += pp[k] * im[k] * pp[k];
     return 0.5 * seg_sum<SEG>(t);
   }
-  __device__ bool criterion(const double (&psm)[NCH], const double (&psp)[NCH], const double (&rho)[NCH]) const {
+  __device__ __forceinline__ bool criterion(const double (&psm)[NCH], const double (&psp)[NCH], const double (&rho)[NCH]) const {
     double a = 0.0, b = 0.0;
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
@@ -231,25 +241,25 @@ struct NutsChain {
     b = seg_sum<SEG>(b);
     return a > 0 && b > 0;
   }
-  __device__ double uniform() {
+  __device__ __forceinline__ double uniform() {
     const uint32_t it = (uint32_t)(iv[I_ITER] + A.iter_offset);
     return uniform_at(A.seed, rid, it, (uint32_t)iv[I_UK]++, TAG_UNI);
   }
-  __device__ void sample_momentum(uint32_t c1, uint32_t c2hi, uint32_t tag) {
+  __device__ __forceinline__ void sample_momentum(uint32_t c1, uint32_t c2hi, uint32_t tag) {
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       const int e = k * SEG + lane;
       p[k] = ok(k) ? normal_at(A.seed, rid, c1, c2hi, (uint32_t)e, tag) / sqrt(im[k]) : 0.0;
     }
   }
-  __device__ void load_sample_point() {
+  __device__ __forceinline__ void load_sample_point() {
     ld(vp(V_QS), q);
     ld(vp(V_GS), g);
     s[S_V] = s[S_VS];
   }
 
   // Request = the new q after begin_update_p + update_q (expl_leapfrog).
-  __device__ void begin_leapfrog(double eps) {
+  __device__ __forceinline__ void begin_leapfrog(double eps) {
     s[S_LFEPS] = eps;
     const double he = 0.5 * eps;
 #pragma unroll
@@ -258,7 +268,7 @@ struct NutsChain {
       q[k] += eps * (im[k] * p[k]);
     }
   }
-  __device__ void finish_leapfrog(double lp, const double (&glp)[NCH]) {
+  __device__ __forceinline__ void finish_leapfrog(double lp, const double (&glp)[NCH]) {
     const double he = 0.5 * s[S_LFEPS];
     s[S_V] = -lp;
 #pragma unroll
@@ -269,7 +279,7 @@ struct NutsChain {
   }
 
   // ---- init_stepsize (base_hmc) as a probe sequence, one leapfrog per step
-  __device__ bool start_probe() {
+  __device__ __forceinline__ bool start_probe() {
     const double e = s[S_NOMEPS];
     if (e == 0 || e > 1e7 || isnan(e)) return false;
     iv[I_PROBE] = 0;
@@ -282,7 +292,7 @@ struct NutsChain {
   }
 
   // ---- adaptation (stepsize_adaptation, windowed var_adaptation)
-  __device__ void learn_stepsize(double adapt_stat) {
+  __device__ __forceinline__ void learn_stepsize(double adapt_stat) {
     s[S_DA_CNT] += 1.0;
     adapt_stat = adapt_stat > 1 ? 1 : adapt_stat;
     const double eta = 1.0 / (s[S_DA_CNT] + A.t0);
@@ -292,7 +302,7 @@ struct NutsChain {
     s[S_XBAR] = (1.0 - x_eta) * s[S_XBAR] + x_eta * x;
     s[S_NOMEPS] = exp(x);
   }
-  __device__ bool learn_variance() {
+  __device__ __forceinline__ bool learn_variance() {
     const unsigned cnt = (unsigned)iv[I_WCNT];
     const unsigned nw = (unsigned)A.num_warmup;
     const bool in_window = (cnt >= A.init_buffer) && (cnt < nw - A.term_buffer) && (cnt != nw);
@@ -343,7 +353,7 @@ struct NutsChain {
   }
 
   // ---- transitions
-  __device__ void begin_subtree() {
+  __device__ __forceinline__ void begin_subtree() {
     iv[I_DIR] = uniform() > 0.5 ? 1 : -1;
     const int f = iv[I_DIR] > 0;
     ld(vp(f ? V_QF : V_QB), q);
@@ -354,7 +364,7 @@ struct NutsChain {
     begin_leapfrog(iv[I_DIR] * s[S_EPS]);
   }
 
-  __device__ void start_transition() {
+  __device__ __forceinline__ void start_transition() {
     iv[I_MODE] = M_TRAJ;
     s[S_EPS] = s[S_NOMEPS];   // base_hmc::sample_stepsize; jitter on its own stream (TAG_JIT)
     if (A.jitter > 0)
@@ -385,14 +395,14 @@ struct NutsChain {
 
   // After a transition (or its adaptation probes): stop, pause or go on.  Returns true
   // if a gradient request was issued.
-  __device__ bool continue_or_stop(int pause_at) {
+  __device__ __forceinline__ bool continue_or_stop(int pause_at) {
     if (iv[I_ITER] >= A.total_iters) { iv[I_MODE] = M_DONE; return false; }
     if (iv[I_ITER] >= pause_at) { iv[I_MODE] = M_PAUSED; return false; }
     start_transition();
     return true;
   }
 
-  __device__ bool end_transition(int pause_at) {
+  __device__ __forceinline__ bool end_transition(int pause_at) {
     const double accept = s[S_SUMMETRO] / (double)iv[I_NLEAP];
     const int it = iv[I_ITER];
     if (it >= A.ud_first) {
@@ -435,7 +445,7 @@ struct NutsChain {
     return continue_or_stop(pause_at);
   }
 
-  __device__ void finish_window_update() {
+  __device__ __forceinline__ void finish_window_update() {
     s[S_MU] = log(10.0 * s[S_NOMEPS]);
     s[S_DA_CNT] = 0.0;
     s[S_SBAR] = 0.0;
@@ -443,7 +453,7 @@ struct NutsChain {
     if (iv[I_SSREASON] == 2) s[S_NOMEPS] = exp(s[S_XBAR]);
   }
 
-  __device__ bool on_probe(double lp, const double (&glp)[NCH], int pause_at) {
+  __device__ __forceinline__ bool on_probe(double lp, const double (&glp)[NCH], int pause_at) {
     finish_leapfrog(lp, glp);
     double h = s[S_V] + kinetic(p);
     if (isnan(h)) h = INFINITY;
@@ -476,7 +486,7 @@ struct NutsChain {
     return continue_or_stop(pause_at);
   }
 
-  __device__ bool on_leaf(double lp, const double (&glp)[NCH], int pause_at) {
+  __device__ __forceinline__ bool on_leaf(double lp, const double (&glp)[NCH], int pause_at) {
     finish_leapfrog(lp, glp);
     if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_LEAP] += 1;
     const double H0 = s[S_H0];
@@ -573,7 +583,8 @@ struct NutsChain {
     st(vp(fwd ? V_QF : V_QB), q);
     st(vp(fwd ? V_PF : V_PB), p);
     st(vp(fwd ? V_GF : V_GB), g);
-    s[fwd ? S_VF : S_VB] = s[S_V];
+    if (fwd) s[S_VF] = s[S_V];            // (no run-time index into the register arrays: that
+    else s[S_VB] = s[S_V];                //  would move them to scratch)
     iv[I_DEPTH] = depth + 1;
     const double u = uniform();
     if (c_lsw > s[S_LSW] || u < exp(c_lsw - s[S_LSW])) {
@@ -622,7 +633,7 @@ struct NutsChain {
   }
 
   // Consume the evaluation requested last step.  Returns true if a new request (at q) was issued.
-  __device__ bool consume(double lp, const double (&glp)[NCH], int pause_at) {
+  __device__ __forceinline__ bool consume(double lp, const double (&glp)[NCH], int pause_at) {
     switch (iv[I_MODE]) {
       case M_INIT: {
         s[S_V] = -lp;
@@ -641,7 +652,7 @@ struct NutsChain {
     }
   }
 
-  __device__ bool resume(int pause_at) {   // PAUSED -> next transition
+  __device__ __forceinline__ bool resume(int pause_at) {   // PAUSED -> next transition
     if (iv[I_MODE] != M_PAUSED) return false;
     return continue_or_stop(pause_at);
   }

@@ -460,7 +460,6 @@ constexpr int S3_W = 8;           // waves per block
 constexpr int S3_MAXP = 7;        // pieces per lane in the forward: K <= 56
 constexpr int S3_KMAX = 52;       // pieces per row (d/2) handled by v3
 
-typedef __attribute__((address_space(3))) void* lds_vptr;
 
 // DPP lane exchange of a double (full-rate VALU, no LDS round trip like ds_bpermute).
 template <int CTRL>
@@ -495,15 +494,6 @@ __device__ __forceinline__ void softplus_terms(double x, double* lp_term, double
 // One wave's ring slot: 8 rows of X (8 * 16 * K bytes) + 8 rows of y (<= 64 B), 16-B aligned.
 __host__ __device__ constexpr int sweep3_slot_bytes(int K) { return 8 * 16 * K + 64; }
 
-// Buffer descriptor built from readfirstlane'd inputs, so the compiler can prove it
-// wave-uniform and keeps it in SGPRs (no waterfall loop around every buffer op).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int64_t bytes) {
-  const uint64_t a = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
-}
 
 // ABL (micro-benchmark ablations only, tools/sweep_micro.hip; 0 in the product): bit 0 replaces
 // the residual's transcendentals by a linear stand-in, bit 1 skips the backward, bit 2 the forward.
