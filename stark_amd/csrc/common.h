@@ -114,6 +114,11 @@ struct NutsArgs {
   int uturn_ext;         // nuts_criterion: 1 = Stan >= 2.23 extra U-turn checks
 };
 
+// Stack vectors per level in use: the Stan >= 2.23 junction checks need SV_PB / SV_PE / SV_PSE,
+// Stan 2.19 only the first four (the smaller stride keeps the fused 8-schools kernel's LDS
+// image, and with it its occupancy, at the 2.19 size).
+__host__ __device__ inline int stack_vecs(const NutsArgs& A) { return A.uturn_ext ? SV_COUNT : SV_PB; }
+
 // RNG stream of a chain: global shard index * chains + chain.
 __host__ __device__ inline uint32_t rng_stream(const NutsArgs& A, int gid) {
   const int s = gid / A.C;

@@ -183,7 +183,7 @@ struct NutsChain {
   __device__ __forceinline__ bool ok(int k) const { return k * SEG + lane < D; }
   __device__ __forceinline__ double* vp(int v) const { return vec + (size_t)v * A.Dp; }
   __device__ __forceinline__ double* svp(int level, int v) const {
-    return stk + ((size_t)level * SV_COUNT + v) * A.Dp;
+    return stk + ((size_t)level * stack_vecs(A) + v) * A.Dp;
   }
   __device__ __forceinline__ void ld(const double* base, double (&r)[NCH]) const {
 #pragma unroll
@@ -737,10 +737,10 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   const int gid = blockIdx.x * CPW + seg;
   const bool live = gid < A.nchains;
   extern __shared__ double fl_all[];
-  const size_t nv = (size_t)V_COUNT * A.Dp, ns = (size_t)A.max_depth * SV_COUNT * A.Dp;
+  const size_t nv = (size_t)V_COUNT * A.Dp, ns = (size_t)A.max_depth * stack_vecs(A) * A.Dp;
   double* const fl = fl_all + (size_t)seg * (nv + ns);
   double* const gvec = A.vec + (size_t)gid * nv;
-  double* const gstk = A.stk + (size_t)gid * ns;
+  double* const gstk = A.stk + (size_t)gid * A.max_depth * SV_COUNT * A.Dp;   // (allocation stride; ns used)
   bool run = live;
   if (run) {
     const int mode0 = A.iv[(size_t)gid * I_COUNT + I_MODE];
@@ -824,7 +824,7 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
 }
 template <int NCH, int CPW, int MINW = 1>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
-  const size_t lds = CPW * sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * SV_COUNT * A.Dp);
+  const size_t lds = CPW * sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp);
   if (lds > 64 * 1024) {
     // the attribute is per device: set it on every launch that needs it (a host call, once per
     // fused launch of up to max_steps leapfrogs) and report a failure as such

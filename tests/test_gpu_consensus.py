@@ -103,8 +103,10 @@ def test_logistic_8_shards_consensus_matches_fulldata_sampler(ctx):
     lm, lc, _ = L.laplace(full, [0], fm, fsd)
     lsd = np.sqrt(np.diag(lc))
     assert np.all(np.abs(fsd / lsd - 1) < 0.1)
-    zl = (cm - lm) / lsd
-    assert np.sqrt(np.mean(zl ** 2)) < 0.25, np.sqrt(np.mean(zl ** 2))
+    # in units of the consensus estimator's batch MCSE, with the Laplace approximation's own
+    # error (O(d / sqrt(N)) sd, ~0.08 here) allowed at 0.1 sd
+    zl = (cm - lm) / np.sqrt((rel * fsd) ** 2 + (0.1 * lsd) ** 2)
+    assert np.mean(zl ** 2) < 2.5, (np.mean(zl ** 2), np.sqrt(np.mean(((cm - lm) / lsd) ** 2)))
     assert pooled.shape[0] == d + 1
     m.close()
     full.close()
