@@ -217,7 +217,8 @@ def main():
 
     nchains = spr * a.chains
     it0 = sampler.iterations()
-    ctx.set_profiling(True)
+    # sweep events on every n-th step (each event pair is a stream barrier: ~1-2 % of a step)
+    ctx.set_profiling(max(1, min(8, K // 16)))
     i0 = sampler.info()
     barrier()
     t0 = time.perf_counter()

@@ -131,7 +131,9 @@ STK_API int stk_ctx_sync(stk_ctx* ctx);
  * null stream, which is torch's default current stream).  The stream is not destroyed with the
  * context. */
 STK_API int stk_ctx_create_on_stream(int device, void* stream, stk_ctx** out);
-STK_API int stk_ctx_set_profiling(stk_ctx* ctx, int on);   /* HIP events around sweeps */
+/* HIP events around the data sweeps of every on-th split-mode step (0: off; 1: every step).
+   Each event pair is a barrier on the stream: sample (e.g. 8) to keep the timing cheap. */
+STK_API int stk_ctx_set_profiling(stk_ctx* ctx, int on);
 STK_API void* stk_ctx_stream(stk_ctx* ctx);                /* hipStream_t of the context */
 
 /* ---- models: stark/stark.py:37-39 + :46 ---- */

@@ -220,6 +220,7 @@ int stk_ctx_sync(stk_ctx* c) {
 
 int stk_ctx_set_profiling(stk_ctx* c, int on) {
   ARG_CHECK(c, "NULL context");
+  ARG_CHECK(on >= 0, "stk_ctx_set_profiling: on must be >= 0");
   c->profiling = on;
   return STK_OK;
 }
@@ -700,7 +701,8 @@ static int run_split_batch(stk_sampler* s, int nsteps, int pause_at) {
   stk_ctx* ctx = m->ctx;
   hipStream_t st = ctx->stream;
   NutsArgs& A = s->A;
-  const bool prof = ctx->profiling != 0;
+  const int every = ctx->profiling;            // events around the sweeps of every n-th step
+  const bool prof = every > 0;
   if (prof) {
     while ((int)s->ev.size() < 2 * nsteps) {
       hipEvent_t e;
@@ -712,13 +714,14 @@ static int run_split_batch(stk_sampler* s, int nsteps, int pause_at) {
   const int step0 = s->step;
   for (int k = 0; k < nsteps; ++k) {
     const int step_id = s->step;
-    if (prof) STK_HIP_CHECK(hipEventRecord(s->ev[2 * k], st));
+    const bool pk = prof && step_id % every == 0;
+    if (pk) STK_HIP_CHECK(hipEventRecord(s->ev[2 * k], st));
     for (const auto& gr : s->groups) {
       STK_HIP_CHECK(stk_launch_sweep(m->family, A.shards, gr.shard0, gr.nsh, m->sh[gr.shard0].n, m->d, gr.T, gr.LD, gr.G, s->Gs, gr.lds,
                                      A.qeval, A.C, A.Dp, s->partial.as<double>(), A.req_step, step_id,
                                      prof ? s->ran.as<int>() : nullptr, st, s->sws.qT ? &s->sws : nullptr));
     }
-    if (prof) STK_HIP_CHECK(hipEventRecord(s->ev[2 * k + 1], st));
+    if (pk) STK_HIP_CHECK(hipEventRecord(s->ev[2 * k + 1], st));
     for (const auto& gr : s->groups) {
       STK_HIP_CHECK(stk_launch_sweep_reduce(m->family, A.shards, gr.shard0, gr.nsh, m->d, gr.G, s->Gs, A.qeval, A.C,
                                             A.Dp, s->partial.as<double>(), A.req_step, step_id, A.lp_in, A.g_in, st));
@@ -739,7 +742,7 @@ static int run_split_batch(stk_sampler* s, int nsteps, int pause_at) {
     STK_HIP_CHECK(hipMemcpyAsync(ran, s->ran.p, sizeof(int) * 64, hipMemcpyDeviceToHost, st));
     STK_HIP_CHECK(hipStreamSynchronize(st));
     for (int k = 0; k < nsteps; ++k) {
-      if (!ran[(step0 + k) & 63]) continue;
+      if ((step0 + k) % every != 0 || !ran[(step0 + k) & 63]) continue;
       float ms = 0.f;
       STK_HIP_CHECK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
       s->sweep_ms += ms;
@@ -772,7 +775,7 @@ int stk_sampler_run(stk_sampler* s, int32_t target_iter, int64_t max_steps) {
       if (max_steps > 0) nb = (int)std::min<int64_t>(nb, max_steps - done_steps);
       RC(run_split_batch(s, nb, pause_at));
       done_steps += nb;
-      batch = std::min(batch * 2, 32);
+      batch = std::min(batch * 2, 64);
     }
   }
   STK_HIP_CHECK(hipStreamSynchronize(ctx->stream));

@@ -72,7 +72,9 @@ class Context:
         if profiling:
             self.set_profiling(True)
 
-    def set_profiling(self, on: bool):
+    def set_profiling(self, on):
+        """HIP events around the data sweeps: False/0 off, True/1 every step, n > 1 every n-th
+        step (the events are stream barriers; sampling keeps them off the step time)."""
         check(_lib.load().stk_ctx_set_profiling(self._h, int(on)))
 
     def sync(self):
