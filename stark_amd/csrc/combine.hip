@@ -186,72 +186,123 @@ __global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t*
 }
 
 // In-place Gauss-Jordan inverse of a batch of SPD P x P matrices (P <= 128), the matrix held
-// in REGISTERS: 1024 threads = 128 columns x 8 row groups, thread (j, g) owns A[g + 8 r][j],
-// r < 16.  Step k needs row k and column k as they stood after step k-1; the threads owning
-// elements of row / column k+1 publish them into the other half of a double-buffered LDS
-// pair while they update, so each step costs one barrier.  Shard b with used[b] == 0 (NaN
-// draws) gets W = 0 and no status; status[b] = 1 when a pivot is <= 0 or NaN (singular
-// covariance: numpy's inv raises LinAlgError).
-constexpr int SI_R = 16;
-__global__ __launch_bounds__(1024) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
-                                                      int32_t* status) {
-  __shared__ double rowk[2][128];
-  __shared__ double colk[2][128];
+// in REGISTERS: 256 threads, thread (bi, bj) owns the 8 x 8 block A[8 bi + u][8 bj + v] of the
+// matrix padded to 128 x 128 with an identity block.  The matrix is first equilibrated to unit
+// diagonal (A = D^1/2 C D^1/2, inv(A) = D^-1/2 inv(C) D^-1/2), so every pivot of C lies in
+// (0, 1].  Step k is then ONE fused rank-1 update of every element, a_ij -= c_i r_j, with the
+// pivot row and column folded in:
+//   c_i = a_ik (i != k), c_k = a_kk - 1;   r_j = a_kj / a_kk (j != k), r_k = 1 + 1/a_kk
+// gives a_kj / a_kk on row k, -a_ik / a_kk on column k and 1/a_kk at (k, k) -- the Gauss-Jordan
+// step -- with no per-element special cases (with pivots <= 1 the folded terms do not cancel).
+// Per step a thread reads its 8 c's and 8 r's (four ds_read_b128 each) and does 64 FMAs; the
+// owners of row / column k+1 publish them (c_{k+1} already folded) into the other half of a
+// double-buffered LDS pair while they update, so each step costs one barrier of 4 waves.
+// (1024 threads with a column and 16 rows each spent 1.4-1.5 us per step on their 16 waves'
+// LDS broadcasts and barrier: 150 us at P = 102.)  Shard b with used[b] == 0 (NaN draws) gets
+// W = 0 and no status; status[b] = 1 when a pivot is <= 0 or NaN (singular covariance: numpy's
+// inv raises LinAlgError).
+constexpr int SI_B = 8;                           // block edge
+__global__ __launch_bounds__(256) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
+                                                     int32_t* status) {
+  __shared__ __attribute__((aligned(16))) double rowk[2][128];
+  __shared__ __attribute__((aligned(16))) double colk[2][128];
+  __shared__ double dsc[128];                     // 1 / sqrt(A_ii)
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int j = tid & 127, g = uniform_int(tid >> 7);   // g: wave-uniform row group
+  const int bi = tid >> 4, bj = tid & 15;        // block row / column
+  const int i0 = SI_B * bi, j0 = SI_B * bj;
   const double* M = Min + (size_t)b * P * P;
   double* out = Out + (size_t)b * P * P;
   if (used && !used[b]) {
-    for (int i = tid; i < P * P; i += 1024) out[i] = 0.0;
+    for (int i = tid; i < P * P; i += 256) out[i] = 0.0;
     if (tid == 0) status[b] = 0;
     return;
   }
-  // padded to 128 x 128 with an identity block: padding rows/columns have zero coupling, so
-  // the P pivot steps leave them untouched and no element needs a bounds test in the loop
-  double a[SI_R];
+  int sing = 0;
+  if (tid < 128) {
+    const double dii = tid < P ? M[(size_t)tid * P + tid] : 1.0;
+    if (!(dii > 0.0)) sing = 1;
+    dsc[tid] = dii > 0.0 ? 1.0 / sqrt(dii) : 1.0;
+  }
+  sing = __syncthreads_or(sing);
+  if (sing) {
+    if (tid == 0) status[b] = 1;
+    return;
+  }
+  double a[SI_B][SI_B];
+  double si[SI_B], sj[SI_B];
 #pragma unroll
-  for (int r = 0; r < SI_R; ++r) {
-    const int i = g + 8 * r;
-    a[r] = (i < P && j < P) ? M[(size_t)i * P + j] : (i == j ? 1.0 : 0.0);
-    if (i == 0) rowk[0][j] = a[r];
-    if (j == 0) colk[0][i] = a[r];
+  for (int u = 0; u < SI_B; ++u) {
+    si[u] = dsc[i0 + u];
+    sj[u] = dsc[j0 + u];
+  }
+#pragma unroll
+  for (int u = 0; u < SI_B; ++u)
+#pragma unroll
+    for (int v = 0; v < SI_B; ++v) {
+      const int i = i0 + u, j = j0 + v;
+      a[u][v] = (i == j) ? 1.0 : ((i < P && j < P) ? M[(size_t)i * P + j] * si[u] * sj[v] : 0.0);
+    }
+  if (bi == 0) {
+#pragma unroll
+    for (int v = 0; v < SI_B; ++v) rowk[0][j0 + v] = a[0][v];
+  }
+  if (bj == 0) {
+#pragma unroll
+    for (int u = 0; u < SI_B; ++u) colk[0][i0 + u] = (i0 + u == 0) ? a[u][0] - 1.0 : a[u][0];
   }
   __syncthreads();
-  int sing = 0;
   for (int k = 0; k < P; ++k) {
     const int cur = k & 1, nxt = cur ^ 1;
+    double c[SI_B], r[SI_B];
+    const dbl2* cp = reinterpret_cast<const dbl2*>(&colk[cur][i0]);
+    const dbl2* rp = reinterpret_cast<const dbl2*>(&rowk[cur][j0]);
+#pragma unroll
+    for (int h = 0; h < SI_B / 2; ++h) {
+      const dbl2 cv = cp[h], rv = rp[h];
+      c[2 * h] = cv.x;
+      c[2 * h + 1] = cv.y;
+      r[2 * h] = rv.x;
+      r[2 * h + 1] = rv.y;
+    }
     const double piv = rowk[cur][k];
     if (!(piv > 0.0)) { sing = 1; break; }      // uniform: every thread read the same pivot
     double ip = __builtin_amdgcn_rcp(piv);      // 1/piv to the last ulp: two Newton steps
     ip = fma(ip, fma(-piv, ip, 1.0), ip);
     ip = fma(ip, fma(-piv, ip, 1.0), ip);
-    const double rj = rowk[cur][j] * ip;
-    double ci[SI_R];
+    const int kb = k >> 3, kv = k & 7;
 #pragma unroll
-    for (int r = 0; r < SI_R; ++r) ci[r] = colk[cur][g + 8 * r];   // broadcast reads
+    for (int v = 0; v < SI_B; ++v) r[v] = (bj == kb && v == kv) ? 1.0 + ip : r[v] * ip;
 #pragma unroll
-    for (int r = 0; r < SI_R; ++r) a[r] = fma(-ci[r], rj, a[r]);   // the rank-1 update: 1 FMA per element
-    if (j == k) {                                                  // column k: one lane
+    for (int u = 0; u < SI_B; ++u)
 #pragma unroll
-      for (int r = 0; r < SI_R; ++r) a[r] = -ci[r] * ip;
+      for (int v = 0; v < SI_B; ++v) a[u][v] = fma(-c[u], r[v], a[u][v]);   // the whole step
+    // publish row and column k+1 (block-uniform tests on k)
+    const int k1 = k + 1, k1b = k1 >> 3, k1u = k1 & 7;
+    if (bi == k1b) {
+#pragma unroll
+      for (int u = 0; u < SI_B; ++u)
+        if (u == k1u) {
+#pragma unroll
+          for (int v = 0; v < SI_B; ++v) rowk[nxt][j0 + v] = a[u][v];
+        }
     }
+    if (bj == k1b) {
 #pragma unroll
-    for (int r = 0; r < SI_R; ++r) {
-      const int i = g + 8 * r;                                     // wave-uniform tests
-      if (i == k) a[r] = (j == k) ? ip : rj;
-      if (i == k + 1) rowk[nxt][j] = a[r];
-    }
-    if (j == k + 1) {
+      for (int v = 0; v < SI_B; ++v)
+        if (v == k1u) {
 #pragma unroll
-      for (int r = 0; r < SI_R; ++r) colk[nxt][g + 8 * r] = a[r];
+          for (int u = 0; u < SI_B; ++u) colk[nxt][i0 + u] = (i0 + u == k1) ? a[u][v] - 1.0 : a[u][v];
+        }
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int r = 0; r < SI_R; ++r) {
-    const int i = g + 8 * r;
-    if (i < P && j < P) out[(size_t)i * P + j] = a[r];
-  }
+  for (int u = 0; u < SI_B; ++u)
+#pragma unroll
+    for (int v = 0; v < SI_B; ++v) {
+      const int i = i0 + u, j = j0 + v;
+      if (i < P && j < P) out[(size_t)i * P + j] = a[u][v] * si[u] * sj[v];
+    }
   if (tid == 0) status[b] = sing;
 }
 
@@ -368,7 +419,7 @@ static bool lds_inverse_fits(int P) { return P <= 128; }
 hipError_t stk_launch_spd_inverse(const double* M, double* Inv, double* work, int P, int batch, const int32_t* used,
                                   int32_t* status, hipStream_t st) {
   if (lds_inverse_fits(P)) {
-    hipLaunchKernelGGL(k_spd_inverse, dim3(batch), dim3(1024), 0, st, M, Inv, P, used, status);
+    hipLaunchKernelGGL(k_spd_inverse, dim3(batch), dim3(256), 0, st, M, Inv, P, used, status);
   } else {
     hipLaunchKernelGGL(k_gj_inverse, dim3(batch), dim3(1024), 0, st, M, work, Inv, P, used, status);
   }
