@@ -52,8 +52,9 @@ def parse():
     p.add_argument("--shards", type=int, default=8)
     p.add_argument("--chains", type=int, default=16,
                    help="chains per shard; they share one data sweep (16: the fp64 MFMA sweep, X.[beta_1..beta_16])")
-    p.add_argument("--adapt-iters", type=int, default=150,
-                   help="Stan warmup iterations (>= 150: a metric window after the initial transient)")
+    p.add_argument("--adapt-iters", type=int, default=None,
+                   help="Stan warmup iterations; default 150 for logistic (the driver's lease) and Stan's 1000 for "
+                        "linear (150 leaves one 50-draw metric window inside the initial transient: DESIGN.md 4)")
     p.add_argument("--stepsize-jitter", type=float, default=0.5,
                    help="Stan control stepsize_jitter; breaks the trajectory-length resonance of NUTS on "
                         "this near-isotropic posterior (DESIGN.md section 4)")
@@ -135,6 +136,8 @@ def _cpu_worker(d, seconds, w, family="logistic"):
 
 def main():
     a = parse()
+    if a.adapt_iters is None:
+        a.adapt_iters = 150 if a.family == "logistic" else 1000
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     # STARK_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N-rank path on one

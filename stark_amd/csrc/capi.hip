@@ -36,13 +36,10 @@ hipError_t stk_launch_gen_shard(double* X, double* yd, int32_t* yi, int64_t nrow
                                 hipStream_t st);
 hipError_t stk_launch_consensus_products(const double* X, int nshards, int P, int S, const int32_t* blk, double* mean,
                                          int32_t* rowbad, int32_t* used, int32_t* status, double* cov, double* W,
-                                         double* work, double* sum_w, double* sum_wtheta, double* partial,
-                                         hipStream_t st);
+                                         double* work, double* sum_w, double* sum_wtheta, hipStream_t st);
 hipError_t stk_launch_consensus_solve(const double* sum_w, const double* sum_wtheta, int P, int S, double* inv_buf,
-                                      double* work, int32_t* status, double* out, double* partial, size_t partial_elems,
-                                      hipStream_t st);
+                                      double* work, int32_t* status, double* out, hipStream_t st);
 size_t stk_spd_inverse_work_bytes(int P, int batch);
-size_t stk_combine_partial_elems(int nshards, int P, int S);
 
 // ---------------------------------------------------------------- errors
 static thread_local char g_err[1024] = "";
@@ -981,12 +978,11 @@ int stk_transition(stk_model* m, int shard, double* q, int32_t C, uint64_t seed,
 }
 
 // ---------------------------------------------------------------- consensus combine
-// Device buffers of one combine (ctx scratch 8..11): the whole chain runs on the context's
+// Device buffers of one combine (ctx scratch 8..10): the whole chain runs on the context's
 // stream with one host synchronisation at the end (combine.hip header).
 namespace {
 struct CombineBufs {
-  double *X, *mean, *cov, *W, *work, *sw, *swt, *inv, *out, *partial;
-  size_t npartial;
+  double *X, *mean, *cov, *W, *work, *sw, *swt, *inv, *out;
   int32_t *rowbad, *used, *status, *blk;
 };
 int combine_bufs(stk_ctx* ctx, int nshards, int P, int S, CombineBufs* b) {
@@ -996,9 +992,6 @@ int combine_bufs(stk_ctx* ctx, int nshards, int P, int S, CombineBufs* b) {
   RC(B[8].ensure(sizeof(double) * (per * nshards + per * 2 + (size_t)P * nshards)));
   RC(B[9].ensure(sizeof(double) * (pp * nshards * 2 + pp * 2) + wk + 16));
   RC(B[10].ensure(sizeof(int32_t) * ((size_t)P * nshards + 2 * (size_t)nshards + 2 + (size_t)P) + 64));
-  b->npartial = stk_combine_partial_elems(nshards, P, S);
-  RC(B[11].ensure(sizeof(double) * b->npartial));
-  b->partial = B[11].as<double>();
   b->X = B[8].as<double>();
   b->swt = b->X + per * nshards;
   b->out = b->swt + per;
@@ -1043,10 +1036,9 @@ int consensus_run(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P,
   STK_HIP_CHECK(hipMemcpyAsync(b.X, draws, sizeof(double) * per * nshards, hipMemcpyDefault, st));
   if (row_block) STK_HIP_CHECK(hipMemcpyAsync(b.blk, row_block, sizeof(int32_t) * P, hipMemcpyDefault, st));
   STK_HIP_CHECK(stk_launch_consensus_products(b.X, nshards, P, S, row_block ? b.blk : nullptr, b.mean, b.rowbad,
-                                              b.used, b.status, b.cov, b.W, b.work, b.sw, b.swt, b.partial, st));
+                                              b.used, b.status, b.cov, b.W, b.work, b.sw, b.swt, st));
   if (out)
-    STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status + nshards, b.out, b.partial,
-                                             b.npartial, st));
+    STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status + nshards, b.out, st));
   std::vector<int32_t> h(2 * nshards + 1, 0);
   STK_HIP_CHECK(hipMemcpyAsync(h.data(), b.used, sizeof(int32_t) * (2 * nshards + (out ? 1 : 0)), hipMemcpyDeviceToHost, st));
   STK_HIP_CHECK(hipStreamSynchronize(st));
@@ -1078,7 +1070,7 @@ int stk_consensus_solve(stk_ctx* ctx, const double* sum_w, const double* sum_wth
   RC(combine_bufs(ctx, 1, P, S, &b));
   STK_HIP_CHECK(hipMemcpyAsync(b.sw, sum_w, sizeof(double) * P * P, hipMemcpyDefault, st));
   STK_HIP_CHECK(hipMemcpyAsync(b.swt, sum_wtheta, sizeof(double) * per, hipMemcpyDefault, st));
-  STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status, b.out, b.partial, b.npartial, st));
+  STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status, b.out, st));
   int32_t hs = 0;
   STK_HIP_CHECK(hipMemcpyAsync(&hs, b.status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
   STK_HIP_CHECK(hipMemcpyAsync(out, b.out, sizeof(double) * per, hipMemcpyDefault, st));

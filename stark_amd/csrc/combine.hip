@@ -9,7 +9,7 @@
 //
 // The whole combine is a handful of launches on one stream, no host round trip in between:
 //   k_row_stats      per (shard, row): mean over the S draws (np.cov centres rows) + NaN flag
-//   k_gemm64<Cov>    cov_s = (X_s - m_s)(X_s - m_s)^T / (S - 1), centring folded into the
+//   k_mgemm<Cov>     cov_s = (X_s - m_s)(X_s - m_s)^T / (S - 1), centring folded into the
 //                    tile loads; rows of different weight blocks (lp__ alone)
 //                    get 0, so the weights are block-diagonal when asked for
 //   k_spd_inverse    W_s = inv(cov_s): in-place Gauss-Jordan on the matrix held in LDS
@@ -19,12 +19,11 @@
 //                    (LinAlgError).  One workgroup per shard, shards in parallel.  P > 128
 //                    falls back to k_gj_inverse (partial pivoting, global memory).
 //   k_sum_w          sum_s W_s in shard order (NaN shards hold W = 0)
-//   k_gemm64<WTheta> sum_s W_s theta_s as ONE GEMM with K = shards x P:
+//   k_mgemm<WTheta>  sum_s W_s theta_s as ONE GEMM with K = shards x P:
 //                    [W_1 .. W_S] (P x SP) . [theta_1; ..; theta_S] (SP x S), NaN shards skipped
-//   k_spd_inverse + k_gemm64<Plain>  out = inv(sum W) . sum W theta
-// k_gemm64: 64 x 64 output tile per 256-thread block, 4 x 4 outputs per thread (rows
-// ty + 16 i, columns tx + 16 j), 16-deep K slices staged in LDS; each output sums its K
-// terms in index order.
+//   k_spd_inverse + k_mgemm<Plain>  out = inv(sum W) . sum W theta
+// k_mgemm: fp64 MFMA, one 16 x 16 NB output tile per block, K split over the block's waves,
+// every output a fixed-order sum (cov_s only on the upper tiles, stored both ways).
 #include "common.h"
 #include <math.h>
 #include <algorithm>
@@ -32,8 +31,7 @@
 namespace stk {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
-constexpr int CB_T = 64;     // output tile
-constexpr int CB_K = 16;     // K slice
+typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 // ---- tile loaders: a(m, k), b(k, n), store(m, n, v)
 struct CovLd {               // batch = shard (blockIdx.z)
@@ -72,83 +70,88 @@ struct PlainLd {             // C[M x N] = A[M x K] . B[K x N], row-major
   __device__ void store(int, int m, int n, double v) const { C[(size_t)m * ldc + n] = v; }
 };
 
-// 64 x 64 tile, K range [kb, ke) of this block's split (blockIdx.z = split * batch + z).
-// The next K slice is loaded into registers while the current one is multiplied.  With a
-// partial buffer the raw sums go to partial[split][z][M][N] and k_splitk_reduce adds the
-// splits in split order (so every output's K terms are summed in a fixed order).
-template <class LD>
-__global__ __launch_bounds__(256) void k_gemm64(LD L, int M, int N, int K, int batch, int kchunk, double* partial) {
-  __shared__ double As[CB_K][CB_T + 1];
-  __shared__ double Bs[CB_K][CB_T + 1];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int m0 = blockIdx.y * CB_T, n0 = blockIdx.x * CB_T;
-  const int z = blockIdx.z % batch, split = blockIdx.z / batch;
-  const int kb = split * kchunk, ke = min(K, kb + kchunk);
-  double acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
-  double ra[4], rb[4];
-  auto fetch = [&](int k0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {        // A slice: 64 rows x 16 k
-      const int e = threadIdx.x + 256 * r;
-      const int m = m0 + (e >> 4), k = k0 + (e & 15);
-      ra[r] = (m < M && k < ke) ? L.a(z, m, k) : 0.0;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {        // B slice: 16 k x 64 columns
-      const int e = threadIdx.x + 256 * r;
-      const int n = n0 + (e & 63), k = k0 + (e >> 6);
-      rb[r] = (n < N && k < ke) ? L.b(z, k, n) : 0.0;
-    }
-  };
-  if (kb < ke) fetch(kb);
-  for (int k0 = kb; k0 < ke; k0 += CB_K) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = threadIdx.x + 256 * r;
-      As[e & 15][e >> 4] = ra[r];
-      Bs[e >> 6][e & 63] = rb[r];
-    }
-    __syncthreads();
-    if (k0 + CB_K < ke) fetch(k0 + CB_K);
-#pragma unroll
-    for (int kk = 0; kk < CB_K; ++kk) {
-      double av[4], bv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = As[kk][ty + 16 * i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = Bs[kk][tx + 16 * j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fma(av[i], bv[j], acc[i][j]);
-    }
-    __syncthreads();
+// fp64 MFMA GEMM for the combine's products (v_mfma_f64_16x16x4_f64).  One block = MG_KW waves
+// = one 16 x (16 NB) output tile; the waves split K into contiguous runs of 16-deep k-groups, and
+// a k-group is 4 MFMAs of k = 4 where lane (r = lane & 15, g = lane >> 4) supplies k = 16 grp +
+// 4 g + j to MFMA j: A(m0 + r, k) and B(k, n0 + r), so each lane's A loads are 4 consecutive k of
+// one row.  The products are small (K <= a few thousand) and their operands come from L2 or the
+// MALL, so the kernel is load-latency bound: a wave issues the loads of CH k-groups at once
+// (4 CH (1 + NB) independent loads in flight) before their MFMAs, and 16 waves per block keep the
+// chains short (<= 2 chunks at the headline size).  Then every wave parks its tile in LDS and
+// the block sums the waves in wave order: each output is a fixed-order sum, independent of the
+// launch.  Out-of-range m, n, k read 0.
+// Blocks are placed XCD-aware: the (z, tile) work list, z-major and column-tile-major, is cut
+// into 8 contiguous ranges and range x runs on XCD x (block id = x + 8 i; dispatch round-robins
+// block ids over the 8 XCDs), so a shard's draws (cov_s) or a column slice of theta (sum W theta,
+// the final solve) stay in one XCD's L2.
+// SYM (square tiles, NB = 1): the tiles of each z are the pairs tm <= tn of a symmetric product
+// and each tile is also stored transposed.
+constexpr int MG_KW = 16;                         // waves per block (K split)
+template <class LD, int NB, int CH, bool SYM>
+__global__ __launch_bounds__(64 * MG_KW) void k_mgemm(LD L, int M, int N, int K, int tiles_m, int tiles_n,
+                                                      int ntiles, int total, int per_xcd) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int item = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+  if (item >= total) return;                      // block-uniform
+  const int z = item / ntiles;
+  int t = item - z * ntiles, tm, tn;
+  if (SYM) {                                      // t -> (tm, tn), tm <= tn, row by row
+    tm = 0;
+    while (t >= tiles_m - tm) { t -= tiles_m - tm; ++tm; }
+    tn = tm + t;
+  } else {                                        // column-tile-major
+    tn = t / tiles_m;
+    tm = t - tn * tiles_m;
   }
+  const int m0 = 16 * tm, n0 = 16 * NB * tn;
+  const int ngrp = (K + 15) >> 4;
+  const int gb = (ngrp * w) / MG_KW, ge = (ngrp * (w + 1)) / MG_KW;
+  const int ma = m0 + r;
+  dbl4 acc[NB];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = dbl4{0.0, 0.0, 0.0, 0.0};
+  for (int c0 = gb; c0 < ge; c0 += CH) {
+    double a[CH][4], b[CH][NB][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + ty + 16 * i, n = n0 + tx + 16 * j;
-      if (m < M && n < N) {
-        if (partial) partial[(((size_t)split * batch + z) * M + m) * N + n] = acc[i][j];
-        else L.store(z, m, n, acc[i][j]);
+    for (int h = 0; h < CH; ++h) {
+      const int k = 16 * (c0 + h) + 4 * g;
+      const bool live = c0 + h < ge;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[h][j] = (live && ma < M && k + j < K) ? L.a(z, ma, k + j) : 0.0;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int n = n0 + 16 * nb + r;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[h][nb][j] = (live && n < N && k + j < K) ? L.b(z, k + j, n) : 0.0;
       }
     }
-}
-
-template <class LD>
-__global__ void k_splitk_reduce(LD L, int M, int N, int batch, int splits, const double* partial) {
-  const size_t tot = (size_t)batch * M * N;
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
-    double v = partial[e];
-    for (int sp = 1; sp < splits; ++sp) v += partial[(size_t)sp * tot + e];
-    const int z = (int)(e / ((size_t)M * N));
-    const size_t r = e % ((size_t)M * N);
-    L.store(z, (int)(r / N), (int)(r % N), v);
+#pragma unroll
+    for (int h = 0; h < CH; ++h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) acc[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[h][j], b[h][nb][j], acc[nb], 0, 0, 0);
+  }
+  __shared__ dbl4 red[MG_KW][NB][64];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) red[w][nb][lane] = acc[nb];
+  __syncthreads();
+  // thread t < 256: lane t & 63 of register i = t >> 6, every column tile
+  if (threadIdx.x < 256) {
+    const int ol = threadIdx.x & 63, i = threadIdx.x >> 6;
+    const int m = m0 + (ol >> 4) + 4 * i;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      double v = red[0][nb][ol][i];
+#pragma unroll
+      for (int ww = 1; ww < MG_KW; ++ww) v += red[ww][nb][ol][i];
+      const int n = n0 + 16 * nb + (ol & 15);
+      if (m < M && n < N) {
+        L.store(z, m, n, v);
+        if (SYM && tm != tn) L.store(z, n, m, v);
+      }
+    }
   }
 }
 
@@ -389,23 +392,13 @@ __global__ void k_sum_w(const double* src, int nshards, size_t n, double* dst) {
   }
 }
 
-// split K so that the grid has >= ~256 blocks of >= 8 slices each (the K loop is latency-bound)
-template <class LD>
-static hipError_t gemm64(const LD& L, int M, int N, int K, int batch, double* partial, size_t partial_elems,
-                         hipStream_t st) {
-  const int tiles = ((N + CB_T - 1) / CB_T) * ((M + CB_T - 1) / CB_T) * batch;
-  const int slices = (K + CB_K - 1) / CB_K;
-  int splits = std::max(1, std::min(std::min(slices / 8, (256 + tiles - 1) / tiles), 32));
-  if (!partial || (size_t)splits * batch * M * N > partial_elems) splits = 1;
-  const int kchunk = ((slices + splits - 1) / splits) * CB_K;
-  splits = (K + kchunk - 1) / kchunk;
-  dim3 grid((N + CB_T - 1) / CB_T, (M + CB_T - 1) / CB_T, batch * splits);
-  hipLaunchKernelGGL(k_gemm64<LD>, grid, dim3(256), 0, st, L, M, N, K, batch, kchunk, splits > 1 ? partial : nullptr);
-  if (splits > 1) {
-    const size_t tot = (size_t)batch * M * N;
-    hipLaunchKernelGGL(k_splitk_reduce<LD>, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 2048)), dim3(256), 0, st,
-                       L, M, N, batch, splits, partial);
-  }
+template <class LD, int NB, int CH, bool SYM>
+static hipError_t mgemm(const LD& L, int M, int N, int K, int batch, hipStream_t st) {
+  const int tiles_m = (M + 15) / 16, tiles_n = SYM ? tiles_m : (N + 16 * NB - 1) / (16 * NB);
+  const int ntiles = SYM ? tiles_m * (tiles_m + 1) / 2 : tiles_m * tiles_n;
+  const int total = ntiles * batch, per_xcd = (total + 7) / 8;
+  hipLaunchKernelGGL((k_mgemm<LD, NB, CH, SYM>), dim3(8 * per_xcd), dim3(64 * MG_KW), 0, st, L, M, N, K, tiles_m,
+                     tiles_n, ntiles, total, per_xcd);
   return hipGetLastError();
 }
 
@@ -428,34 +421,27 @@ hipError_t stk_launch_spd_inverse(const double* M, double* Inv, double* work, in
 size_t stk_spd_inverse_work_bytes(int P, int batch) {
   return lds_inverse_fits(P) ? 0 : sizeof(double) * (size_t)P * 2 * P * batch;
 }
-// split-K partial sums: up to 32 splits of the largest GEMM of a combine
-size_t stk_combine_partial_elems(int nshards, int P, int S) {
-  return (size_t)32 * std::max((size_t)nshards * P * P, (size_t)P * S);
-}
 
 // draws X [nshards][P][S] on the device -> W [nshards][P][P], sum_w [P][P], sum_wtheta [P][S].
 hipError_t stk_launch_consensus_products(const double* X, int nshards, int P, int S, const int32_t* blk, double* mean,
                                          int32_t* rowbad, int32_t* used, int32_t* status, double* cov, double* W,
-                                         double* work, double* sum_w, double* sum_wtheta, double* partial,
-                                         hipStream_t st) {
-  const size_t pe = stk_combine_partial_elems(nshards, P, S);
+                                         double* work, double* sum_w, double* sum_wtheta, hipStream_t st) {
   hipLaunchKernelGGL(k_row_stats, dim3(nshards * P), dim3(256), 0, st, X, S, mean, rowbad);
   hipLaunchKernelGGL(k_shard_used, dim3((nshards + 63) / 64), dim3(64), 0, st, rowbad, P, nshards, used);
-  hipError_t e = gemm64(CovLd{X, mean, blk, cov, P, S, 1.0 / (double)(S - 1)}, P, P, S, nshards, partial, pe, st);
+  hipError_t e = mgemm<CovLd, 1, 4, true>(CovLd{X, mean, blk, cov, P, S, 1.0 / (double)(S - 1)}, P, P, S, nshards, st);
   if (e != hipSuccess) return e;
   e = stk_launch_spd_inverse(cov, W, work, P, nshards, used, status, st);
   if (e != hipSuccess) return e;
   const size_t pp = (size_t)P * P;
   hipLaunchKernelGGL(k_sum_w, dim3((unsigned)std::min<size_t>((pp + 255) / 256, 1024)), dim3(256), 0, st, W, nshards,
                      pp, sum_w);
-  return gemm64(WThetaLd{W, X, used, sum_wtheta, P, S}, P, S, nshards * P, 1, partial, pe, st);
+  return mgemm<WThetaLd, 2, 2, false>(WThetaLd{W, X, used, sum_wtheta, P, S}, P, S, nshards * P, 1, st);
 }
 
 // out [P][S] = inv(sum_w) . sum_wtheta (inv_buf [P][P], work for P > 128)
 hipError_t stk_launch_consensus_solve(const double* sum_w, const double* sum_wtheta, int P, int S, double* inv_buf,
-                                      double* work, int32_t* status, double* out, double* partial, size_t partial_elems,
-                                      hipStream_t st) {
+                                      double* work, int32_t* status, double* out, hipStream_t st) {
   hipError_t e = stk_launch_spd_inverse(sum_w, inv_buf, work, P, 1, nullptr, status, st);
   if (e != hipSuccess) return e;
-  return gemm64(PlainLd{inv_buf, sum_wtheta, out, P, S, S}, P, S, P, 1, partial, partial_elems, st);
+  return mgemm<PlainLd, 2, 2, false>(PlainLd{inv_buf, sum_wtheta, out, P, S, S}, P, S, P, 1, st);
 }
