@@ -12,8 +12,8 @@
 //   k_mgemm<Cov>     cov_s = (X_s - m_s)(X_s - m_s)^T / (S - 1), centring folded into the
 //                    tile loads; rows of different weight blocks (lp__ alone)
 //                    get 0, so the weights are block-diagonal when asked for
-//   k_spd_inverse    W_s = inv(cov_s): in-place Gauss-Jordan on the matrix held in LDS
-//                    (P <= 128: 128 KB of the CU's 160), diagonal pivots -- a covariance is
+//   k_spd_inverse    W_s = inv(cov_s): block Gauss-Jordan on 16 x 16 tiles held in registers,
+//                    fp64 MFMA updates (P <= 128), diagonal pivots -- a covariance is
 //                    symmetric positive (semi)definite, where diagonal pivoting is stable
 //                    (Cholesky's argument); a pivot <= 0 or NaN is reported as singular
 //                    (LinAlgError).  One workgroup per shard, shards in parallel.  P > 128
@@ -188,35 +188,39 @@ __global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t*
   used[s] = bad ? 0 : 1;
 }
 
-// In-place Gauss-Jordan inverse of a batch of SPD P x P matrices (P <= 128), the matrix held
-// in REGISTERS: 256 threads, thread (bi, bj) owns the 8 x 8 block A[8 bi + u][8 bj + v] of the
-// matrix padded to 128 x 128 with an identity block.  The matrix is first equilibrated to unit
-// diagonal (A = D^1/2 C D^1/2, inv(A) = D^-1/2 inv(C) D^-1/2), so every pivot of C lies in
-// (0, 1].  Step k is then ONE fused rank-1 update of every element, a_ij -= c_i r_j, with the
-// pivot row and column folded in:
-//   c_i = a_ik (i != k), c_k = a_kk - 1;   r_j = a_kj / a_kk (j != k), r_k = 1 + 1/a_kk
-// gives a_kj / a_kk on row k, -a_ik / a_kk on column k and 1/a_kk at (k, k) -- the Gauss-Jordan
-// step -- with no per-element special cases (with pivots <= 1 the folded terms do not cancel).
-// Per step a thread reads its 8 c's and 8 r's (four ds_read_b128 each) and does 64 FMAs; the
-// owners of row / column k+1 publish them (c_{k+1} already folded) into the other half of a
-// double-buffered LDS pair while they update, so each step costs one barrier of 4 waves.
-// (1024 threads with a column and 16 rows each spent 1.4-1.5 us per step on their 16 waves'
-// LDS broadcasts and barrier: 150 us at P = 102.)  Shard b with used[b] == 0 (NaN draws) gets
-// W = 0 and no status; status[b] = 1 when a pivot is <= 0 or NaN (singular covariance: numpy's
-// inv raises LinAlgError).
-constexpr int SI_B = 8;                           // block edge
-__global__ __launch_bounds__(256) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
+// Inverse of a batch of SPD P x P matrices (P <= 128): block Gauss-Jordan on 16 x 16 tiles with
+// fp64 MFMA, the matrix held in REGISTERS.  One block per matrix, 8 waves; wave w owns tile
+// column w of the matrix padded to NT = ceil(P / 16) tiles with an identity block, each tile in
+// the MFMA D layout (lane (c, g) register i = T[g + 4i][c]).  The matrix is first equilibrated
+// to unit diagonal (A = D^1/2 C D^1/2, inv(A) = D^-1/2 inv(C) D^-1/2), so every scalar pivot,
+// a diagonal of a Schur complement, lies in (0, 1].  Panel kb (pivot block K = tile kb):
+//   Dinv = inv(T(K, K))                    every wave, wave-local Gauss-Jordan (below)
+//   R_J = Dinv T(K, J),  T(K, J) = R_J     owner of column J != kb: 4 MFMAs
+//   T(I, J) -= T(I, K) R_J                 4 MFMAs per tile
+//   T(I, K) = -T(I, K) Dinv,  T(K, K) = Dinv   owner of column kb
+// An MFMA contracts 4 k-slots; call s maps slot g to k = g + 4 s, so its B operand is register s
+// of a D-layout tile (R_J, T(K, J)) as is, and its A operand is lane (r, g) holding A[r][g + 4s].
+// The column block T(., K) is read in that A layout from LDS, where the owner of the column
+// publishes it (negated, 4 consecutive doubles per lane) right after its own update of the
+// previous panel, into the other half of a double buffer: ONE barrier per panel (7 at P = 102,
+// against one per pivot).  Dinv (symmetric) is used as its own transpose where a B-layout or
+// D-layout copy is needed (rounding-level difference).  The 16 x 16 inverse: lane (r, g) holds
+// D[r][g + 4s] (s = 0..3); pivot k takes column k and row k with 5 cross-lane shuffles and does
+// the folded rank-1 step a_ij -= c_i r_j (c_k = a_kk - 1, r_k = 1 + 1/a_kk, r_j = a_kj / a_kk:
+// Gauss-Jordan with no per-element cases; with pivots <= 1 the folded terms do not cancel).
+// Shard b with used[b] == 0 (NaN draws) gets W = 0 and no status; status[b] = 1 when a pivot is
+// <= 0 or NaN (singular covariance: numpy's inv raises LinAlgError).
+template <int NT>
+__global__ __launch_bounds__(512) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
                                                      int32_t* status) {
-  __shared__ __attribute__((aligned(16))) double rowk[2][128];
-  __shared__ __attribute__((aligned(16))) double colk[2][128];
-  __shared__ double dsc[128];                     // 1 / sqrt(A_ii)
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int bi = tid >> 4, bj = tid & 15;        // block row / column
-  const int i0 = SI_B * bi, j0 = SI_B * bj;
+  __shared__ __attribute__((aligned(16))) double pub[2][NT][256];   // -T(I, K), A-read order
+  __shared__ double dsc[128];                                        // 1 / sqrt(A_ii)
+  const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lg = lane >> 4;
   const double* M = Min + (size_t)b * P * P;
   double* out = Out + (size_t)b * P * P;
   if (used && !used[b]) {
-    for (int i = tid; i < P * P; i += 256) out[i] = 0.0;
+    for (int i = tid; i < P * P; i += 512) out[i] = 0.0;
     if (tid == 0) status[b] = 0;
     return;
   }
@@ -231,81 +235,109 @@ __global__ __launch_bounds__(256) void k_spd_inverse(const double* Min, double* 
     if (tid == 0) status[b] = 1;
     return;
   }
-  double a[SI_B][SI_B];
-  double si[SI_B], sj[SI_B];
+  const bool own = w < NT;
+  const int jc = 16 * w + lr;                     // this lane's matrix column
+  dbl4 T[NT];
 #pragma unroll
-  for (int u = 0; u < SI_B; ++u) {
-    si[u] = dsc[i0 + u];
-    sj[u] = dsc[j0 + u];
-  }
+  for (int I = 0; I < NT; ++I)
 #pragma unroll
-  for (int u = 0; u < SI_B; ++u)
-#pragma unroll
-    for (int v = 0; v < SI_B; ++v) {
-      const int i = i0 + u, j = j0 + v;
-      a[u][v] = (i == j) ? 1.0 : ((i < P && j < P) ? M[(size_t)i * P + j] * si[u] * sj[v] : 0.0);
+    for (int i = 0; i < 4; ++i) {
+      const int row = 16 * I + lg + 4 * i;
+      T[I][i] = (row == jc) ? 1.0 : ((own && row < P && jc < P) ? M[(size_t)row * P + jc] * dsc[row] * dsc[jc] : 0.0);
     }
-  if (bi == 0) {
+  // publish: lane (c, g) register i = T[g + 4i][c] goes to row g + 4i, position (c & 3) * 4 + (c >> 2),
+  // so that reader lane (r, g) finds T[r][g + 4s], s = 0..3, as 4 consecutive doubles
+  auto publish = [&](double* dst) {
 #pragma unroll
-    for (int v = 0; v < SI_B; ++v) rowk[0][j0 + v] = a[0][v];
-  }
-  if (bj == 0) {
+    for (int I = 0; I < NT; ++I)
 #pragma unroll
-    for (int u = 0; u < SI_B; ++u) colk[0][i0 + u] = (i0 + u == 0) ? a[u][0] - 1.0 : a[u][0];
-  }
+      for (int i = 0; i < 4; ++i) dst[I * 256 + (lg + 4 * i) * 16 + (lr & 3) * 4 + (lr >> 2)] = -T[I][i];
+  };
+  if (w == 0) publish(&pub[0][0][0]);
   __syncthreads();
-  for (int k = 0; k < P; ++k) {
-    const int cur = k & 1, nxt = cur ^ 1;
-    double c[SI_B], r[SI_B];
-    const dbl2* cp = reinterpret_cast<const dbl2*>(&colk[cur][i0]);
-    const dbl2* rp = reinterpret_cast<const dbl2*>(&rowk[cur][j0]);
+  for (int kb = 0; kb < NT; ++kb) {
+    const int cur = kb & 1;
+    // -T(I, K) in A layout: lane (r, g) reads -T(I,K)[r][g + 4s], s = 0..3, as two 16-B words
+    auto cn = [&](int I, double* v) {
+      const dbl2* src = reinterpret_cast<const dbl2*>(&pub[cur][I][lr * 16 + lg * 4]);
+      const dbl2 x0 = src[0], x1 = src[1];
+      v[0] = x0.x;
+      v[1] = x0.y;
+      v[2] = x1.x;
+      v[3] = x1.y;
+    };
+    double a[4];                                  // D = T(K, K) in A layout, then Dinv
+    cn(kb, a);
 #pragma unroll
-    for (int h = 0; h < SI_B / 2; ++h) {
-      const dbl2 cv = cp[h], rv = rp[h];
-      c[2 * h] = cv.x;
-      c[2 * h + 1] = cv.y;
-      r[2 * h] = rv.x;
-      r[2 * h + 1] = rv.y;
+    for (int s = 0; s < 4; ++s) a[s] = -a[s];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int kg = k & 3, ks = k >> 2;
+      const double c = __shfl(a[ks], lr + 16 * kg);        // a[r][k]
+      double rk[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) rk[s] = __shfl(a[s], k + 16 * lg);   // a[k][g + 4s]
+      const double piv = __shfl(a[ks], k + 16 * kg);       // a[k][k], uniform
+      if (!(piv > 0.0)) sing = 1;
+      double ip = __builtin_amdgcn_rcp(piv);
+      ip = fma(ip, fma(-piv, ip, 1.0), ip);
+      ip = fma(ip, fma(-piv, ip, 1.0), ip);
+      const double cc = (lr == k) ? c - 1.0 : c;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double rj = (lg + 4 * s == k) ? 1.0 + ip : rk[s] * ip;
+        a[s] = fma(-cc, rj, a[s]);
+      }
     }
-    const double piv = rowk[cur][k];
-    if (!(piv > 0.0)) { sing = 1; break; }      // uniform: every thread read the same pivot
-    double ip = __builtin_amdgcn_rcp(piv);      // 1/piv to the last ulp: two Newton steps
-    ip = fma(ip, fma(-piv, ip, 1.0), ip);
-    ip = fma(ip, fma(-piv, ip, 1.0), ip);
-    const int kb = k >> 3, kv = k & 7;
+    if (sing) break;                              // uniform: every wave inverted the same block
+    if (own) {
+      if (w == kb) {
 #pragma unroll
-    for (int v = 0; v < SI_B; ++v) r[v] = (bj == kb && v == kv) ? 1.0 + ip : r[v] * ip;
+        for (int I = 0; I < NT; ++I) {
+          if (I == kb) {
+            T[I] = dbl4{a[0], a[1], a[2], a[3]};
+          } else {
+            double c[4];
+            cn(I, c);
+            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int u = 0; u < SI_B; ++u)
-#pragma unroll
-      for (int v = 0; v < SI_B; ++v) a[u][v] = fma(-c[u], r[v], a[u][v]);   // the whole step
-    // publish row and column k+1 (block-uniform tests on k)
-    const int k1 = k + 1, k1b = k1 >> 3, k1u = k1 & 7;
-    if (bi == k1b) {
-#pragma unroll
-      for (int u = 0; u < SI_B; ++u)
-        if (u == k1u) {
-#pragma unroll
-          for (int v = 0; v < SI_B; ++v) rowk[nxt][j0 + v] = a[u][v];
+            for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(c[s], a[s], acc, 0, 0, 0);
+            T[I] = acc;
+          }
         }
-    }
-    if (bj == k1b) {
+      } else {
+        dbl4 tk = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int v = 0; v < SI_B; ++v)
-        if (v == k1u) {
+        for (int I = 0; I < NT; ++I)
+          if (I == kb) tk = T[I];
+        dbl4 R = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int u = 0; u < SI_B; ++u) colk[nxt][i0 + u] = (i0 + u == k1) ? a[u][v] - 1.0 : a[u][v];
+        for (int s = 0; s < 4; ++s) R = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], tk[s], R, 0, 0, 0);
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+          if (I == kb) {
+            T[I] = R;
+          } else {
+            double c[4];
+            cn(I, c);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) T[I] = __builtin_amdgcn_mfma_f64_16x16x4f64(c[s], R[s], T[I], 0, 0, 0);
+          }
         }
+      }
+      if (w == kb + 1) publish(&pub[cur ^ 1][0][0]);
     }
     __syncthreads();
   }
+  if (own && !sing) {
 #pragma unroll
-  for (int u = 0; u < SI_B; ++u)
+    for (int I = 0; I < NT; ++I)
 #pragma unroll
-    for (int v = 0; v < SI_B; ++v) {
-      const int i = i0 + u, j = j0 + v;
-      if (i < P && j < P) out[(size_t)i * P + j] = a[u][v] * si[u] * sj[v];
-    }
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * I + lg + 4 * i;
+        if (row < P && jc < P) out[(size_t)row * P + jc] = T[I][i] * dsc[row] * dsc[jc];
+      }
+  }
   if (tid == 0) status[b] = sing;
 }
 
@@ -412,7 +444,13 @@ static bool lds_inverse_fits(int P) { return P <= 128; }
 hipError_t stk_launch_spd_inverse(const double* M, double* Inv, double* work, int P, int batch, const int32_t* used,
                                   int32_t* status, hipStream_t st) {
   if (lds_inverse_fits(P)) {
-    hipLaunchKernelGGL(k_spd_inverse, dim3(batch), dim3(256), 0, st, M, Inv, P, used, status);
+    const int nt = (P + 15) / 16;
+    switch (nt) {
+#define STK_INV(N) \
+  case N: hipLaunchKernelGGL(k_spd_inverse<N>, dim3(batch), dim3(512), 0, st, M, Inv, P, used, status); break;
+      STK_INV(1) STK_INV(2) STK_INV(3) STK_INV(4) STK_INV(5) STK_INV(6) STK_INV(7) STK_INV(8)
+#undef STK_INV
+    }
   } else {
     hipLaunchKernelGGL(k_gj_inverse, dim3(batch), dim3(1024), 0, st, M, work, Inv, P, used, status);
   }

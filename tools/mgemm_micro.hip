@@ -57,13 +57,20 @@ int main() {
   hipMemcpy(used, u.data(), sizeof(int32_t) * Z, hipMemcpyHostToDevice);
   hipStream_t st = 0;
   printf("cov  CovLd   %8.2f us\n", timeit([&] { mgemm<CovLd, 1, 4, true>(CovLd{X, mean, nullptr, cov, P, S, 1.0}, P, P, S, Z, st); }));
+  mgemm<CovLd, 1, 4, true>(CovLd{X, mean, nullptr, cov, P, S, 1.0 / (S - 1)}, P, P, S, Z, st);
+  int32_t* status;
+  hipMalloc(&status, sizeof(int32_t) * Z);
+  printf("inv  spd x1  %8.2f us\n", timeit([&] { stk_launch_spd_inverse(cov, W, nullptr, P, 1, nullptr, status, st); }, 20));
+  printf("inv  spd x8  %8.2f us\n", timeit([&] { stk_launch_spd_inverse(cov, W, nullptr, P, Z, used, status, st); }, 20));
+  int32_t hs[8];
+  hipMemcpy(hs, status, sizeof(hs), hipMemcpyDeviceToHost);
+  printf("inv  status  %d %d %d %d %d %d %d %d\n", hs[0], hs[1], hs[2], hs[3], hs[4], hs[5], hs[6], hs[7]);
   printf("cov  RowLd   %8.2f us\n", timeit([&] { mgemm<RowLd, 1, 4, true>(RowLd{X, cov, P, S}, P, P, S, Z, st); }));
   printf("cov  SynthLd %8.2f us\n", timeit([&] { mgemm<SynthLd, 1, 4, true>(SynthLd{cov, P}, P, P, S, Z, st); }));
   printf("wth  WTheta  %8.2f us\n", timeit([&] { mgemm<WThetaLd, 2, 2, false>(WThetaLd{W, X, used, out, P, S}, P, S, Z * P, 1, st); }));
   printf("wth  Plain   %8.2f us\n", timeit([&] { mgemm<PlainLd, 2, 2, false>(PlainLd{W, X, out, Z * P, S, S}, P, S, Z * P, 1, st); }));
   printf("wth  Synth   %8.2f us\n", timeit([&] { mgemm<SynthLd, 2, 2, false>(SynthLd{out, S}, P, S, Z * P, 1, st); }));
   printf("sol  Plain   %8.2f us\n", timeit([&] { mgemm<PlainLd, 2, 2, false>(PlainLd{W, X, out, P, S, S}, P, S, P, 1, st); }));
-  printf("inv  spd     %8.2f us\n", timeit([&] { stk_launch_spd_inverse(cov, W, nullptr, P, 1, nullptr, used, st); }, 10));
   printf("empty launch %8.2f us\n", timeit([&] { hipLaunchKernelGGL(k_sum_w, dim3(1), dim3(64), 0, st, mean, 1, (size_t)1, mean + 1); }));
   return 0;
 }
