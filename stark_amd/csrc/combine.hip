@@ -194,27 +194,55 @@ __global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t*
 // the MFMA D layout (lane (c, g) register i = T[g + 4i][c]).  The matrix is first equilibrated
 // to unit diagonal (A = D^1/2 C D^1/2, inv(A) = D^-1/2 inv(C) D^-1/2), so every scalar pivot,
 // a diagonal of a Schur complement, lies in (0, 1].  Panel kb (pivot block K = tile kb):
-//   Dinv = inv(T(K, K))                    every wave, wave-local Gauss-Jordan (below)
 //   R_J = Dinv T(K, J),  T(K, J) = R_J     owner of column J != kb: 4 MFMAs
 //   T(I, J) -= T(I, K) R_J                 4 MFMAs per tile
 //   T(I, K) = -T(I, K) Dinv,  T(K, K) = Dinv   owner of column kb
-// An MFMA contracts 4 k-slots; call s maps slot g to k = g + 4 s, so its B operand is register s
-// of a D-layout tile (R_J, T(K, J)) as is, and its A operand is lane (r, g) holding A[r][g + 4s].
-// The column block T(., K) is read in that A layout from LDS, where the owner of the column
-// publishes it (negated, 4 consecutive doubles per lane) right after its own update of the
-// previous panel, into the other half of a double buffer: ONE barrier per panel (7 at P = 102,
-// against one per pivot).  Dinv (symmetric) is used as its own transpose where a B-layout or
-// D-layout copy is needed (rounding-level difference).  The 16 x 16 inverse: lane (r, g) holds
-// D[r][g + 4s] (s = 0..3); pivot k takes column k and row k with 5 cross-lane shuffles and does
-// the folded rank-1 step a_ij -= c_i r_j (c_k = a_kk - 1, r_k = 1 + 1/a_kk, r_j = a_kj / a_kk:
-// Gauss-Jordan with no per-element cases; with pivots <= 1 the folded terms do not cancel).
-// Shard b with used[b] == 0 (NaN draws) gets W = 0 and no status; status[b] = 1 when a pivot is
-// <= 0 or NaN (singular covariance: numpy's inv raises LinAlgError).
+// with Dinv = inv(T(K, K)).  An MFMA contracts 4 k-slots; call s maps slot g to k = g + 4 s, so
+// its B operand is register s of a D-layout tile (R_J, T(K, J)) as is, and its A operand is lane
+// (r, g) holding A[r][g + 4s].  The column block T(., K) is read in that A layout from LDS.
+// Look-ahead: in panel kb the owner of column kb + 1 updates its pivot tile T(kb+1, kb+1) first,
+// inverts it (16 x 16, below) while its other tiles' MFMAs are in flight, and publishes the
+// updated column (negated, 4 consecutive doubles per lane) together with its Dinv into the other
+// half of a double buffer -- so each panel costs ONE barrier (7 at P = 102, against one per
+// pivot) and the small inverse sits on one wave's path instead of every wave's.  A symmetric
+// matrix is used as its own transpose where the other layout is needed (T(K, K) read in the A
+// layout, Dinv as a B operand and as the D-layout T(K, K)): rounding-level differences.
+// The 16 x 16 inverse: lane (r, g) holds D[r][g + 4s] (s = 0..3); pivot k takes column k and row
+// k with cross-lane shuffles and does the folded rank-1 step a_ij -= c_i r_j (c_k = a_kk - 1,
+// r_k = 1 + 1/a_kk, r_j = a_kj / a_kk: Gauss-Jordan with no per-element cases; with pivots <= 1
+// the folded terms do not cancel).  Shard b with used[b] == 0 (NaN draws) gets W = 0 and no
+// status; status[b] = 1 when a pivot is <= 0 or NaN (singular covariance: numpy's inv raises
+// LinAlgError).
+__device__ __forceinline__ int inv16(double (&a)[4], int lr, int lg) {
+  int sing = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int kg = k & 3, ks = k >> 2;
+    const double c = __shfl(a[ks], lr + 16 * kg);          // a[r][k]
+    double rk[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) rk[s] = __shfl(a[s], k + 16 * lg);   // a[k][g + 4s]
+    const double piv = __shfl(a[ks], k + 16 * kg);         // a[k][k], wave-uniform
+    if (!(piv > 0.0)) sing = 1;
+    double ip = __builtin_amdgcn_rcp(piv);
+    ip = fma(ip, fma(-piv, ip, 1.0), ip);
+    ip = fma(ip, fma(-piv, ip, 1.0), ip);
+    const double cc = (lr == k) ? c - 1.0 : c;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const double rj = (lg + 4 * s == k) ? 1.0 + ip : rk[s] * ip;
+      a[s] = fma(-cc, rj, a[s]);
+    }
+  }
+  return sing;
+}
+
 template <int NT>
 __global__ __launch_bounds__(512) void k_spd_inverse(const double* Min, double* Out, int P, const int32_t* used,
                                                      int32_t* status) {
-  __shared__ __attribute__((aligned(16))) double pub[2][NT][256];   // -T(I, K), A-read order
-  __shared__ double dsc[128];                                        // 1 / sqrt(A_ii)
+  __shared__ __attribute__((aligned(16))) double pub[2][NT + 1][256];  // -T(I, K) then Dinv, A-read order
+  __shared__ int32_t psing[2];
+  __shared__ double dsc[128];                                           // 1 / sqrt(A_ii)
   const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
   const double* M = Min + (size_t)b * P * P;
@@ -245,51 +273,41 @@ __global__ __launch_bounds__(512) void k_spd_inverse(const double* Min, double* 
       const int row = 16 * I + lg + 4 * i;
       T[I][i] = (row == jc) ? 1.0 : ((own && row < P && jc < P) ? M[(size_t)row * P + jc] * dsc[row] * dsc[jc] : 0.0);
     }
-  // publish: lane (c, g) register i = T[g + 4i][c] goes to row g + 4i, position (c & 3) * 4 + (c >> 2),
-  // so that reader lane (r, g) finds T[r][g + 4s], s = 0..3, as 4 consecutive doubles
-  auto publish = [&](double* dst) {
+  // slot I < NT: lane (c, g) register i = -T(I)[g + 4i][c] goes to row g + 4i, position
+  // (c & 3) * 4 + (c >> 2), so that reader lane (r, g) finds -T(I)[r][g + 4s], s = 0..3, as 4
+  // consecutive doubles; slot NT: Dinv, written by lane (r, g) in its own A layout
+  auto publish = [&](double* dst, const double (&dinv)[4], int sg) {
 #pragma unroll
     for (int I = 0; I < NT; ++I)
 #pragma unroll
       for (int i = 0; i < 4; ++i) dst[I * 256 + (lg + 4 * i) * 16 + (lr & 3) * 4 + (lr >> 2)] = -T[I][i];
+    dbl2* dp = reinterpret_cast<dbl2*>(dst + NT * 256 + lr * 16 + lg * 4);
+    dp[0] = dbl2{dinv[0], dinv[1]};
+    dp[1] = dbl2{dinv[2], dinv[3]};
+    if (lane == 0) psing[(dst == &pub[0][0][0]) ? 0 : 1] = sg;
   };
-  if (w == 0) publish(&pub[0][0][0]);
+  auto rd4 = [&](const double* src, double (&v)[4]) {
+    const dbl2* p = reinterpret_cast<const dbl2*>(src + lr * 16 + lg * 4);
+    const dbl2 x0 = p[0], x1 = p[1];
+    v[0] = x0.x;
+    v[1] = x0.y;
+    v[2] = x1.x;
+    v[3] = x1.y;
+  };
+  if (w == 0) {
+    double d0[4] = {T[0][0], T[0][1], T[0][2], T[0][3]};   // T(0, 0), symmetric: read as A layout
+    const int sg = inv16(d0, lr, lg);
+    publish(&pub[0][0][0], d0, sg);
+  }
   __syncthreads();
   for (int kb = 0; kb < NT; ++kb) {
     const int cur = kb & 1;
-    // -T(I, K) in A layout: lane (r, g) reads -T(I,K)[r][g + 4s], s = 0..3, as two 16-B words
-    auto cn = [&](int I, double* v) {
-      const dbl2* src = reinterpret_cast<const dbl2*>(&pub[cur][I][lr * 16 + lg * 4]);
-      const dbl2 x0 = src[0], x1 = src[1];
-      v[0] = x0.x;
-      v[1] = x0.y;
-      v[2] = x1.x;
-      v[3] = x1.y;
-    };
-    double a[4];                                  // D = T(K, K) in A layout, then Dinv
-    cn(kb, a);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) a[s] = -a[s];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int kg = k & 3, ks = k >> 2;
-      const double c = __shfl(a[ks], lr + 16 * kg);        // a[r][k]
-      double rk[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) rk[s] = __shfl(a[s], k + 16 * lg);   // a[k][g + 4s]
-      const double piv = __shfl(a[ks], k + 16 * kg);       // a[k][k], uniform
-      if (!(piv > 0.0)) sing = 1;
-      double ip = __builtin_amdgcn_rcp(piv);
-      ip = fma(ip, fma(-piv, ip, 1.0), ip);
-      ip = fma(ip, fma(-piv, ip, 1.0), ip);
-      const double cc = (lr == k) ? c - 1.0 : c;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const double rj = (lg + 4 * s == k) ? 1.0 + ip : rk[s] * ip;
-        a[s] = fma(-cc, rj, a[s]);
-      }
+    if (psing[cur]) {
+      sing = 1;
+      break;                                      // block-uniform
     }
-    if (sing) break;                              // uniform: every wave inverted the same block
+    double a[4];                                  // Dinv(kb), A layout
+    rd4(&pub[cur][NT][0], a);
     if (own) {
       if (w == kb) {
 #pragma unroll
@@ -298,7 +316,7 @@ __global__ __launch_bounds__(512) void k_spd_inverse(const double* Min, double* 
             T[I] = dbl4{a[0], a[1], a[2], a[3]};
           } else {
             double c[4];
-            cn(I, c);
+            rd4(&pub[cur][I][0], c);
             dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(c[s], a[s], acc, 0, 0, 0);
@@ -313,19 +331,45 @@ __global__ __launch_bounds__(512) void k_spd_inverse(const double* Min, double* 
         dbl4 R = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int s = 0; s < 4; ++s) R = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], tk[s], R, 0, 0, 0);
+        if (w == kb + 1) {                        // look-ahead: the next pivot tile first, then its inverse
+          double d[4];
 #pragma unroll
-        for (int I = 0; I < NT; ++I) {
-          if (I == kb) {
-            T[I] = R;
-          } else {
-            double c[4];
-            cn(I, c);
+          for (int I = 0; I < NT; ++I)
+            if (I == kb + 1) {
+              double c[4];
+              rd4(&pub[cur][I][0], c);
 #pragma unroll
-            for (int s = 0; s < 4; ++s) T[I] = __builtin_amdgcn_mfma_f64_16x16x4f64(c[s], R[s], T[I], 0, 0, 0);
+              for (int s = 0; s < 4; ++s) T[I] = __builtin_amdgcn_mfma_f64_16x16x4f64(c[s], R[s], T[I], 0, 0, 0);
+#pragma unroll
+              for (int s = 0; s < 4; ++s) d[s] = T[I][s];
+            }
+          const int sg = inv16(d, lr, lg);
+#pragma unroll
+          for (int I = 0; I < NT; ++I) {
+            if (I == kb) {
+              T[I] = R;
+            } else if (I != kb + 1) {
+              double c[4];
+              rd4(&pub[cur][I][0], c);
+#pragma unroll
+              for (int s = 0; s < 4; ++s) T[I] = __builtin_amdgcn_mfma_f64_16x16x4f64(c[s], R[s], T[I], 0, 0, 0);
+            }
+          }
+          publish(&pub[cur ^ 1][0][0], d, sg);
+        } else {
+#pragma unroll
+          for (int I = 0; I < NT; ++I) {
+            if (I == kb) {
+              T[I] = R;
+            } else {
+              double c[4];
+              rd4(&pub[cur][I][0], c);
+#pragma unroll
+              for (int s = 0; s < 4; ++s) T[I] = __builtin_amdgcn_mfma_f64_16x16x4f64(c[s], R[s], T[I], 0, 0, 0);
+            }
           }
         }
       }
-      if (w == kb + 1) publish(&pub[cur ^ 1][0][0]);
     }
     __syncthreads();
   }
