@@ -34,10 +34,10 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_PEAK_TFS = 78.6    # MI355X fp64 matrix (= vector) spec, dense
-FP64_MFMA_MEASURED_TFS = 47.9   # v_mfma_f64_16x16x4 back to back, 4 waves/SIMD, clock-stamped at 2.38 GHz
-                                # (tools/mfma_ceiling.hip, profiles/r02b_mfma_ceiling.log): the instruction the sweep issues
-FP64_MFMA4_MEASURED_TFS = 75.2  # v_mfma_f64_4x4x4_4b back to back (profiles/r02n_mfma4.log): the chip's fp64 ceiling;
-                                # the sweep cannot feed it ("the four-block form")
+FP64_MFMA_MEASURED_TFS = 78.0   # v_mfma_f64_16x16x4 back to back (64 cycles per SIMD), clock-stamped at 2.38 GHz,
+                                # built with -mllvm -amdgpu-mfma-vgpr-form (tools/mfma_ceiling.hip,
+                                # profiles/r02zd_mfma_ceiling_vgprform.log): the instruction the sweep issues
+FP64_MFMA4_MEASURED_TFS = 75.8  # v_mfma_f64_4x4x4_4b back to back (profiles/r02zd_mfma_ceiling_vgprform.log)
 
 
 def parse():
