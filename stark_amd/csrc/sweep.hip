@@ -1854,9 +1854,28 @@ __global__ __launch_bounds__(256) void k_qt_swizzle(SweepArgs A, int d) {
   *reinterpret_cast<double*>(img + g5_chain_off(k, c)) = v;
 }
 
-// Pass F: one block per (shard, chunk); the chunk's 64-row tiles one after another.
+// Both passes: one block of G5_NW = 8 waves per CU (two per SIMD); wave w takes row / column
+// group w & 3 (16 rows or columns) and chain half w >> 2 (two 16-chain MFMA tiles), so every
+// output's K terms are summed in the same order as with one wave per group.  The stages run
+// through a ring of G5_NS = 4 LDS slots (128 KB): three stages are in flight while one is
+// consumed, and one barrier per stage both publishes the landed stage and frees the slot read
+// in the previous one (the refill of that slot is issued right after it).
+constexpr int G5_NW = 8;
+constexpr int G5_NS = 4;
+constexpr int G5_DMA = 4;     // DMA instructions per wave per stage (2 for each operand image)
+#ifndef G5_FW
+#define G5_FW 4               // pass F: waves per block (4: two blocks per CU, NS = 2)
+#define G5_FS 2
+#endif
+
+// Pass F: one block per (shard, chunk); the chunk's 64-row tiles one after another.  NW waves
+// (4: two blocks per CU, a double buffer; 8: one block per CU, the 4-stage ring), each with
+// NCT = 16 / NW chain tiles.  With one block per CU every wave reaches the tile epilogue (the
+// residual, VALU) at once and the MFMAs idle meanwhile; two blocks overlap one's epilogue with
+// the other's GEMM, which measured faster for this pass.
 template <int FAM>
-__global__ __launch_bounds__(256, 2) void k_gemm_fwd(SweepArgs A) {
+__global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A) {
+  constexpr int NW = G5_FW, NS = G5_FS, NCT = 16 / NW, NDMA = 16 / NW;
   const int shard = A.shard0 + blockIdx.x / A.G;
   const int chunk = blockIdx.x % A.G;
   if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
@@ -1864,6 +1883,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_fwd(SweepArgs A) {
   const ShardDev sh = A.shards[shard];
   const int d = sh.d, KP = g5_kp(d), NKC = KP / G5_KC;
   const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int wr = w & 3, wc = w >> 2;
   const int lr = lane & 15, lh = lane >> 4;
   const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;
   const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
@@ -1872,17 +1892,18 @@ __global__ __launch_bounds__(256, 2) void k_gemm_fwd(SweepArgs A) {
   const int ntile = (int)(t1 - t0);
 
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  char* const stg = reinterpret_cast<char*>(lds);                 // 2 stages: [X 16 KB][beta^T 16 KB]
-  double* const sptab = reinterpret_cast<double*>(stg + 2 * G5_STAGE);
+  char* const stg = reinterpret_cast<char*>(lds);                 // NS stages: [X 16 KB][beta^T 16 KB]
+  double* const sptab = reinterpret_cast<double*>(stg + NS * G5_STAGE);
   if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
 
-  // per-lane chain constants: chain 16 ct + lr
+  // per-lane chain constants: chain 16 ct + lr, ct = 2 wc + c2
   const double* qb = A.q + (size_t)shard * G5_C * A.Dp;
-  double alpha[4], inv_s[4];
+  double alpha[NCT], inv_s[NCT];
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    alpha[ct] = qb[(size_t)(16 * ct + lr) * A.Dp];
-    inv_s[ct] = (FAM == STK_LINREG) ? exp(-qb[(size_t)(16 * ct + lr) * A.Dp + d + 1]) : 0.0;
+  for (int c2 = 0; c2 < NCT; ++c2) {
+    const int ct = NCT * wc + c2;
+    alpha[c2] = qb[(size_t)(16 * ct + lr) * A.Dp];
+    inv_s[c2] = (FAM == STK_LINREG) ? exp(-qb[(size_t)(16 * ct + lr) * A.Dp + d + 1]) : 0.0;
   }
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(0xF70);
@@ -1890,71 +1911,78 @@ __global__ __launch_bounds__(256, 2) void k_gemm_fwd(SweepArgs A) {
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
   const __amdgpu_buffer_rsrc_t br = uniform_rsrc(A.qT + (size_t)shard * KP * G5_C, (int64_t)KP * G5_C * 8);
   // X stage: slot s (16 B) = row s>>4, piece (s & 15) ^ (row & 15) of the stage's 32 columns
-  int xvo[4];
+  int xvo[NDMA];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int sl = (w * 4 + i) * 64 + lane, row = sl >> 4, pc = (sl & 15) ^ (row & 15);
+  for (int i = 0; i < NDMA; ++i) {
+    const int sl = (w * NDMA + i) * 64 + lane, row = sl >> 4, pc = (sl & 15) ^ (row & 15);
     xvo[i] = row * d * 8 + pc * 16;
   }
   auto issue = [&](int st) {          // global stage index st = tile * NKC + kc
     const int tile = st / NKC, kc = st % NKC;
-    char* b = stg + (st & 1) * G5_STAGE;
+    char* b = stg + (st % NS) * G5_STAGE;
     const int xso = tile * G5_TR * d * 8 + kc * G5_KC * 8;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * 4 + i) * 1024), 16, xvo[i], xso, 0, 0);
+    for (int i = 0; i < NDMA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * NDMA + i) * 1024), 16, xvo[i], xso, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(br, (lds_vptr)(b + 16384 + (w * 4 + i) * 1024), 16, lane * 16,
-                                               kc * G5_KC * 512 + (w * 4 + i) * 1024, 0, 0);
+    for (int i = 0; i < NDMA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(br, (lds_vptr)(b + 16384 + (w * NDMA + i) * 1024), 16, lane * 16,
+                                               kc * G5_KC * 512 + (w * NDMA + i) * 1024, 0, 0);
   };
 
-  double lpa[4] = {0.0, 0.0, 0.0, 0.0}, gaa[4] = {0.0, 0.0, 0.0, 0.0};
+  double lpa[NCT], gaa[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] = gaa[c2] = 0.0;
   char* const Rimg = reinterpret_cast<char*>(A.R + ((size_t)shard * A.Rrows + r0) * G5_C);
   const int nst = ntile * NKC;
-  if (nst > 0) issue(0);
-  dbl4 acc[4];
+  for (int s0 = 0; s0 < NS - 1 && s0 < nst; ++s0) issue(s0);
+  dbl4 acc[NCT];
   for (int st = 0; st < nst; ++st) {
     const int kc = st % NKC;
     if (kc == 0) {
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) acc[ct] = dbl4{0.0, 0.0, 0.0, 0.0};
+      for (int c2 = 0; c2 < NCT; ++c2) acc[c2] = dbl4{0.0, 0.0, 0.0, 0.0};
     }
-    if (st + 1 < nst) { issue(st + 1); wait_vm<8>(); } else { wait_vm<0>(); }
-    __syncthreads();                                     // stage st landed for every wave
-    const char* b = stg + (st & 1) * G5_STAGE;
-    const int r = 16 * w + lr;
+    wait_vmcnt(std::min(NS - 2, nst - 1 - st) * 2 * NDMA);   // own DMAs of stage st retired
+    __syncthreads();                                     // stage st landed for every wave; slot of st-1 free
+    if (st + NS - 1 < nst) issue(st + NS - 1);
+    const char* b = stg + (st % NS) * G5_STAGE;
+    const int r = 16 * wr + lr;
 #pragma unroll
     for (int step = 0; step < G5_KC / 4; ++step) {
       const int kk = 4 * step + lh;
       const double a = *reinterpret_cast<const double*>(b + r * 256 + ((((kk >> 1) ^ (r & 15))) << 4) + ((kk & 1) << 3));
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-        acc[ct] = mfma_f64(a, *reinterpret_cast<const double*>(b + 16384 + g5_chain_off(kk, 16 * ct + lr)), acc[ct]);
+      for (int c2 = 0; c2 < NCT; ++c2)
+        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + 16384 + g5_chain_off(kk, 16 * (NCT * wc + c2) + lr)), acc[c2]);
     }
-    __syncthreads();                                     // reads of this stage done before it is refilled
     if (kc == NKC - 1) {                                 // ---- tile epilogue: residual, R, lp
-      // eta goes through this wave's own 8 KB of the stage just consumed (its DMA slots, which
-      // it refills only after this loop), so the 16 residuals run one at a time from LDS
-      // instead of holding 16 softplus evaluations' temporaries in registers
+      __syncthreads();                                   // every wave is done reading stage st
+      // eta goes through this wave's own 2 NCT KB of the stage just consumed (refilled only
+      // after the next barrier), so the residuals run one at a time from LDS instead of holding
+      // 4 NCT softplus evaluations' temporaries in registers
       const int tile = st / NKC;
-      char* const b2 = stg + (st & 1) * G5_STAGE;
-      auto eslot = [&](int e) -> double* {
-        return reinterpret_cast<double*>(b2 + (e < 8 ? w * 4096 : 16384 + w * 4096) + (e & 7) * 512) + lane;
-      };
+      char* const b2 = stg + (st % NS) * G5_STAGE;
+      auto eslot = [&](int e) -> double* { return reinterpret_cast<double*>(b2 + w * (NCT * 2048) + e * 512) + lane; };
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int c2 = 0; c2 < NCT; ++c2)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) *eslot(ct * 4 + i) = acc[ct][i];
+        for (int i = 0; i < 4; ++i) *eslot(c2 * 4 + i) = acc[c2][i];
 #pragma unroll 1
-      for (int e = 0; e < 16; ++e) {
-        const int ct = e >> 2, i = e & 3;
-        const int row = 16 * w + lh + 4 * i;               // row of the tile
+      for (int e = 0; e < 4 * NCT; ++e) {
+        const int c2 = e >> 2, i = e & 3, ct = NCT * wc + c2;
+        const int row = 16 * wr + lh + 4 * i;              // row of the tile
         const int64_t grow = (int64_t)tile * G5_TR + row;  // row of the chunk
         const bool valid = grow < nrows;
         double yv = 0.0;
         if (valid) yv = (FAM == STK_LOGREG) ? (double)sh.yi[r0 + grow] : sh.y[r0 + grow];
-        const double al = ct == 0 ? alpha[0] : (ct == 1 ? alpha[1] : (ct == 2 ? alpha[2] : alpha[3]));
+        double al = alpha[0], isg = inv_s[0];
+#pragma unroll
+        for (int q = 1; q < NCT; ++q)
+          if (c2 == q) {
+            al = alpha[q];
+            isg = inv_s[q];
+          }
         const double eta = *eslot(e) + al;
         double dv, lt;
         if constexpr (FAM == STK_LOGREG) {
@@ -1965,17 +1993,16 @@ __global__ __launch_bounds__(256, 2) void k_gemm_fwd(SweepArgs A) {
           lt = hi ? -ex : (lo ? ntt : -lm);
           dv = sgn * (hi ? ex : (lo ? 1.0 : wt));
         } else {
-          const double is = ct == 0 ? inv_s[0] : (ct == 1 ? inv_s[1] : (ct == 2 ? inv_s[2] : inv_s[3]));
-          const double z = (yv - eta) * is;
+          const double z = (yv - eta) * isg;
           lt = z * z;
-          dv = z * is;
+          dv = z * isg;
         }
         dv = valid ? dv : 0.0;
         lt = valid ? lt : 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          lpa[q] += q == ct ? lt : 0.0;
-          gaa[q] += q == ct ? dv : 0.0;
+        for (int q = 0; q < NCT; ++q) {
+          lpa[q] += q == c2 ? lt : 0.0;
+          gaa[q] += q == c2 ? dv : 0.0;
         }
         *reinterpret_cast<double*>(Rimg + g5_chain_off((int)grow, 16 * ct + lr)) = dv;
       }
@@ -1983,27 +2010,27 @@ __global__ __launch_bounds__(256, 2) void k_gemm_fwd(SweepArgs A) {
     }
   }
 
-  // ---- lp and sum(d eta) per chain: lanes lr of the 4 row groups of the 4 waves, fixed order
+  // ---- lp and sum(d eta) per chain: lanes lr of the 4 row groups h of the 4 waves wr, fixed order
   __syncthreads();
-  double* red = lds;                                     // [4 waves][64 lanes][4 ct][2]
+  double* red = lds;                                     // [NW waves][64 lanes][NCT][2]
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    red[((w * 64 + lane) * 4 + ct) * 2 + 0] = lpa[ct];
-    red[((w * 64 + lane) * 4 + ct) * 2 + 1] = gaa[ct];
+  for (int c2 = 0; c2 < NCT; ++c2) {
+    red[((w * 64 + lane) * NCT + c2) * 2 + 0] = lpa[c2];
+    red[((w * 64 + lane) * NCT + c2) * 2 + 1] = gaa[c2];
   }
   __syncthreads();
   if (tid < 2 * G5_C) {
-    const int c = tid >> 1, kind = tid & 1, ct = c >> 4, l = c & 15;
+    const int c = tid >> 1, kind = tid & 1, ct = c >> 4, l = c & 15, cw = ct / NCT, c2 = ct % NCT;
     double v = 0.0;
     for (int ww = 0; ww < 4; ++ww)
-      for (int h = 0; h < 4; ++h) v += red[((ww * 64 + h * 16 + l) * 4 + ct) * 2 + kind];
+      for (int h = 0; h < 4; ++h) v += red[(((cw * 4 + ww) * 64 + h * 16 + l) * NCT + c2) * 2 + kind];
     A.partial[(((size_t)shard * A.Gs + chunk) * G5_C + c) * A.PW + (kind == 0 ? d + 1 : 0)] = v;
   }
 }
 
 // Pass B: one block per (shard, chunk, 64-column block); G[j][c] += X[r][j] R[r][c] over the
 // chunk's rows, straight into the chunk's partial row (columns 1 .. d).
-__global__ __launch_bounds__(256, 2) void k_gemm_bwd(SweepArgs A, int njb) {
+__global__ __launch_bounds__(64 * G5_NW, 1) void k_gemm_bwd(SweepArgs A, int njb) {
   // XCD-aware order: blocks are dealt to the 8 XCDs round-robin (blockIdx % 8), so the njb
   // column blocks of a chunk get blockIdx values of one residue -- one XCD, whose L2 then
   // serves the chunk's R rows to all of them (else each XCD re-reads R from HBM)
@@ -2023,6 +2050,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_bwd(SweepArgs A, int njb) {
   const ShardDev sh = A.shards[shard];
   const int d = sh.d;
   const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int wr = w & 3, wc = w >> 2;
   const int lr = lane & 15, lh = lane >> 4;
   const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;
   const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
@@ -2032,53 +2060,51 @@ __global__ __launch_bounds__(256, 2) void k_gemm_bwd(SweepArgs A, int njb) {
   const int j0 = jb * G5_JB;
 
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  char* const stg = reinterpret_cast<char*>(lds);      // 2 stages: [X^T block 16 KB][R block 16 KB]
+  char* const stg = reinterpret_cast<char*>(lds);      // G5_NS stages: [X^T block 16 KB][R block 16 KB]
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
   const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(A.R + ((size_t)shard * A.Rrows + r0) * G5_C, (int64_t)nrows * G5_C * 8);
   // X stage: slot s = row s >> 5, piece (s & 31) ^ ((row & 1) << 3) of the block's 64 columns
-  int xvo[4];
+  int xvo[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int sl = (w * 4 + i) * 64 + lane, row = sl >> 5, pc = (sl & 31) ^ ((row & 1) << 3);
+  for (int i = 0; i < 2; ++i) {
+    const int sl = (w * 2 + i) * 64 + lane, row = sl >> 5, pc = (sl & 31) ^ ((row & 1) << 3);
     xvo[i] = row * d * 8 + (j0 + 2 * pc) * 8;
   }
   auto issue = [&](int st) {
-    char* b = stg + (st & 1) * G5_STAGE;
+    char* b = stg + (st % G5_NS) * G5_STAGE;
     const int xso = st * G5_RB * d * 8;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * 4 + i) * 1024), 16, xvo[i], xso, 0, 0);
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * 2 + i) * 1024), 16, xvo[i], xso, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (lds_vptr)(b + 16384 + (w * 4 + i) * 1024), 16, lane * 16,
-                                               st * G5_RB * 512 + (w * 4 + i) * 1024, 0, 0);
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (lds_vptr)(b + 16384 + (w * 2 + i) * 1024), 16, lane * 16,
+                                               st * G5_RB * 512 + (w * 2 + i) * 1024, 0, 0);
   };
-  dbl4 acc[4];
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) acc[ct] = dbl4{0.0, 0.0, 0.0, 0.0};
-  if (nst > 0) issue(0);
-  const int jl = 16 * w + lr;                          // A row (column of X) of this lane
+  dbl4 acc[2] = {dbl4{0.0, 0.0, 0.0, 0.0}, dbl4{0.0, 0.0, 0.0, 0.0}};
+  for (int s0 = 0; s0 < G5_NS - 1 && s0 < nst; ++s0) issue(s0);
+  const int jl = 16 * wr + lr;                         // A row (column of X) of this lane
   for (int st = 0; st < nst; ++st) {
-    if (st + 1 < nst) { issue(st + 1); wait_vm<8>(); } else { wait_vm<0>(); }
+    wait_vmcnt(std::min(G5_NS - 2, nst - 1 - st) * G5_DMA);
     __syncthreads();
-    const char* b = stg + (st & 1) * G5_STAGE;
+    if (st + G5_NS - 1 < nst) issue(st + G5_NS - 1);
+    const char* b = stg + (st % G5_NS) * G5_STAGE;
 #pragma unroll
     for (int step = 0; step < G5_RB / 4; ++step) {
       const int r = 4 * step + lh;
       const double a = *reinterpret_cast<const double*>(b + r * 512 + ((((jl >> 1) ^ ((r & 1) << 3))) << 4) + ((jl & 1) << 3));
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-        acc[ct] = mfma_f64(a, *reinterpret_cast<const double*>(b + 16384 + g5_chain_off(r, 16 * ct + lr)), acc[ct]);
+      for (int c2 = 0; c2 < 2; ++c2)
+        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + 16384 + g5_chain_off(r, 16 * (2 * wc + c2) + lr)), acc[c2]);
     }
-    __syncthreads();
   }
   double* out = A.partial + ((size_t)shard * A.Gs + chunk) * G5_C * A.PW;
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
+  for (int c2 = 0; c2 < 2; ++c2) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int j = j0 + 16 * w + lh + 4 * i;
-      if (j < d) out[(size_t)(16 * ct + lr) * A.PW + 1 + j] = acc[ct][i];
+      const int j = j0 + 16 * wr + lh + 4 * i;
+      if (j < d) out[(size_t)(16 * (2 * wc + c2) + lr) * A.PW + 1 + j] = acc[c2][i];
     }
   }
 }
@@ -2236,7 +2262,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *T = G5_TR;
     *LD = 0;
     *G = (int)g;
-    *lds_bytes = 2 * G5_STAGE + SP_TAB * sizeof(double);
+    *lds_bytes = G5_FS * G5_STAGE + SP_TAB * sizeof(double);
     return;
   }
   if (var == 4) {
@@ -2459,9 +2485,9 @@ hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, 
     hipLaunchKernelGGL(k_qt_swizzle, dim3((g5_kp(d) * G5_C + 255) / 256, nsh), dim3(256), 0, st, A, d);
     auto kf = family == STK_LOGREG ? k_gemm_fwd<STK_LOGREG> : k_gemm_fwd<STK_LINREG>;
     allow_big_lds((const void*)kf);
-    hipLaunchKernelGGL(kf, dim3(nblocks), dim3(256), lds, st, A);
+    hipLaunchKernelGGL(kf, dim3(nblocks), dim3(64 * G5_FW), lds, st, A);
     allow_big_lds((const void*)k_gemm_bwd);
-    hipLaunchKernelGGL(k_gemm_bwd, dim3(nblocks * njb), dim3(256), 2 * G5_STAGE, st, A, njb);
+    hipLaunchKernelGGL(k_gemm_bwd, dim3(nblocks * njb), dim3(64 * G5_NW), G5_NS * G5_STAGE, st, A, njb);
     return hipGetLastError();
   }
   if (family == STK_LOGREG) return pick_c<STK_LOGREG>(A, n, d, T, nblocks, lds, st);

@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 2 re-entry: the 8-wave, 4-stage-ring full-data GEMM passes -- parity (C = 64 paths), then
+# the per-kernel split at the configs[4] micro geometry
+set -o pipefail
+mkdir -p gpurun_out/r02zh /tmp/mb
+O=gpurun_out/r02zh
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_nuts.py -m gpu -q -x --timeout 300 --timeout-method thread -k "regression_lpgrad or prior_lpgrad or placement or reproducible or fulldata or linear_regression_closed or logistic_matches" > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest.log; [ $rc -le 1 ] || exit 2
+hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/sweep_micro.hip -o /tmp/mb/sw 2>/dev/null || exit 5
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- /tmp/mb/sw 2000000 8 1000 5 64 > $O/micro.log 2>&1 || exit 3
+grep -E "v5|sweep" $O/micro.log
+python3 tools/rocpd_summary.py stats $O/prof/run_results.db > $O/stats.csv 2>&1; head -4 $O/stats.csv

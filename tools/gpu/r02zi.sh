@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 2 re-entry: pass F as 4 waves x 2 blocks/CU (default) vs 8 waves x 4-stage ring; pass B 8 waves
+set -o pipefail
+mkdir -p gpurun_out/r02zi /tmp/mb
+O=gpurun_out/r02zi
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_nuts.py -m gpu -q -x --timeout 300 --timeout-method thread -k "regression_lpgrad or prior_lpgrad or placement or reproducible or fulldata or linear_regression_closed or logistic_matches" > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log; [ $rc -le 1 ] || exit 2
+hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/sweep_micro.hip -o /tmp/mb/sw 2>/dev/null || exit 5
+hipcc -O3 --offload-arch=gfx950 -std=c++17 -DG5_FW=8 -DG5_FS=4 tools/sweep_micro.hip -o /tmp/mb/sw8 2>/dev/null || exit 5
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- /tmp/mb/sw 2000000 8 1000 5 64 > $O/micro.log 2>&1 || exit 3
+grep -E "v5" $O/micro.log
+python3 tools/rocpd_summary.py stats $O/prof/run_results.db > $O/stats.csv 2>&1; head -3 $O/stats.csv
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof8 -o run -- /tmp/mb/sw8 2000000 8 1000 5 64 > $O/micro8.log 2>&1 || exit 3
+grep -E "v5" $O/micro8.log
+python3 tools/rocpd_summary.py stats $O/prof8/run_results.db > $O/stats8.csv 2>&1; head -3 $O/stats8.csv
