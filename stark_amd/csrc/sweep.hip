@@ -1937,15 +1937,24 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
   const int nst = ntile * NKC;
   for (int s0 = 0; s0 < NS - 1 && s0 < nst; ++s0) issue(s0);
   dbl4 acc[NCT];
+  double yt[4] = {0.0, 0.0, 0.0, 0.0};                  // y of this lane's 4 rows of the current tile
   for (int st = 0; st < nst; ++st) {
     const int kc = st % NKC;
     if (kc == 0) {
 #pragma unroll
       for (int c2 = 0; c2 < NCT; ++c2) acc[c2] = dbl4{0.0, 0.0, 0.0, 0.0};
     }
-    wait_vmcnt(std::min(NS - 2, nst - 1 - st) * 2 * NDMA);   // own DMAs of stage st retired
+    wait_vmcnt(std::min(NS - 2, nst - 1 - st) * 2 * NDMA);   // own DMAs of stage st retired (and the y loads)
     __syncthreads();                                     // stage st landed for every wave; slot of st-1 free
     if (st + NS - 1 < nst) issue(st + NS - 1);
+    if (kc == 0) {                                       // the tile's y, needed by its epilogue: one latency per tile
+      const int64_t tb = (int64_t)(st / NKC) * G5_TR + 16 * wr + lh;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t grow = tb + 4 * i;
+        yt[i] = grow < nrows ? ((FAM == STK_LOGREG) ? (double)sh.yi[r0 + grow] : sh.y[r0 + grow]) : 0.0;
+      }
+    }
     const char* b = stg + (st % NS) * G5_STAGE;
     const int r = 16 * wr + lr;
 #pragma unroll
@@ -1974,8 +1983,7 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
         const int row = 16 * wr + lh + 4 * i;              // row of the tile
         const int64_t grow = (int64_t)tile * G5_TR + row;  // row of the chunk
         const bool valid = grow < nrows;
-        double yv = 0.0;
-        if (valid) yv = (FAM == STK_LOGREG) ? (double)sh.yi[r0 + grow] : sh.y[r0 + grow];
+        const double yv = i == 0 ? yt[0] : (i == 1 ? yt[1] : (i == 2 ? yt[2] : yt[3]));
         double al = alpha[0], isg = inv_s[0];
 #pragma unroll
         for (int q = 1; q < NCT; ++q)
