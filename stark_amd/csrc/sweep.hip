@@ -1862,6 +1862,20 @@ __global__ __launch_bounds__(256) void k_qt_swizzle(SweepArgs A, int d) {
 // in the previous one (the refill of that slot is issued right after it).
 constexpr int G5_NW = 8;
 constexpr int G5_NS = 4;
+// A barrier that leaves LDS-DMAs in flight: __syncthreads() makes hipcc drain vmcnt(0) first
+// (an LDS-DMA is a pending LDS write on the VM counter), which would empty the stage ring at
+// every stage; the counted wait before it is what orders the DMA'd data.
+#ifndef G5_RAWBAR
+#define G5_RAWBAR 1
+#endif
+__device__ __forceinline__ void lds_barrier() {
+  if constexpr (G5_RAWBAR) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);                 // lgkmcnt(0): this wave's LDS accesses done
+    __builtin_amdgcn_s_barrier();
+  } else {
+    __syncthreads();
+  }
+}
 constexpr int G5_DMA = 4;     // DMA instructions per wave per stage (2 for each operand image)
 #ifndef G5_FW
 #define G5_FW 4               // pass F: waves per block (4: two blocks per CU, NS = 2)
@@ -1945,7 +1959,7 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
       for (int c2 = 0; c2 < NCT; ++c2) acc[c2] = dbl4{0.0, 0.0, 0.0, 0.0};
     }
     wait_vmcnt(std::min(NS - 2, nst - 1 - st) * 2 * NDMA);   // own DMAs of stage st retired (and the y loads)
-    __syncthreads();                                     // stage st landed for every wave; slot of st-1 free
+    lds_barrier();                                       // stage st landed for every wave; slot of st-1 free
     if (st + NS - 1 < nst) issue(st + NS - 1);
     if (kc == 0) {                                       // the tile's y, needed by its epilogue: one latency per tile
       const int64_t tb = (int64_t)(st / NKC) * G5_TR + 16 * wr + lh;
@@ -1966,7 +1980,7 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
         acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + 16384 + g5_chain_off(kk, 16 * (NCT * wc + c2) + lr)), acc[c2]);
     }
     if (kc == NKC - 1) {                                 // ---- tile epilogue: residual, R, lp
-      __syncthreads();                                   // every wave is done reading stage st
+      lds_barrier();                                     // every wave is done reading stage st
       // eta goes through this wave's own 2 NCT KB of the stage just consumed (refilled only
       // after the next barrier), so the residuals run one at a time from LDS instead of holding
       // 4 NCT softplus evaluations' temporaries in registers
@@ -2094,7 +2108,7 @@ __global__ __launch_bounds__(64 * G5_NW, 1) void k_gemm_bwd(SweepArgs A, int njb
   const int jl = 16 * wr + lr;                         // A row (column of X) of this lane
   for (int st = 0; st < nst; ++st) {
     wait_vmcnt(std::min(G5_NS - 2, nst - 1 - st) * G5_DMA);
-    __syncthreads();
+    lds_barrier();
     if (st + G5_NS - 1 < nst) issue(st + G5_NS - 1);
     const char* b = stg + (st % G5_NS) * G5_STAGE;
 #pragma unroll
