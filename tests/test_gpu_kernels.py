@@ -141,9 +141,10 @@ def test_combine_general_shards(ctx, orc, S):
                                    atol=1e-11 * np.abs(ref).max())
 
 
-@pytest.mark.parametrize("P,S", [(2, 50), (40, 300), (128, 700), (150, 900)])
+@pytest.mark.parametrize("P,S", [(2, 50), (16, 80), (17, 90), (40, 300), (113, 640), (128, 700), (150, 900)])
 def test_combine_sizes_and_blocked_weights(ctx, orc, P, S):
-    """Every inverse path (LDS Gauss-Jordan up to P = 128, global-memory pivoted GJ above)
+    """Every inverse path (register block Gauss-Jordan on 16 x 16 tiles up to P = 128 -- one
+    to eight tiles, full and ragged last tiles -- and the global-memory pivoted GJ above)
     vs the numpy restatement, and the blocked call (stk_consensus_blocked) equal to combining
     the two row blocks separately."""
     from stark_amd import engine
@@ -206,7 +207,7 @@ def test_combine_separate_lp(ctx, orc):
     assert z2(joint[:-1]) > 5.0        # lp__ offsets leak through the cross-covariances (measured 38.6)
 
 
-def test_combine_singular_raises(ctx):
+def test_combine_singular_constant_shards(ctx):
     from stark_amd import engine
     from stark_amd._lib import LinAlgError
     x = np.ones((3, 50))
