@@ -58,8 +58,10 @@ def parse():
     p.add_argument("--stepsize-jitter", type=float, default=0.5,
                    help="Stan control stepsize_jitter; breaks the trajectory-length resonance of NUTS on "
                         "this near-isotropic posterior (DESIGN.md section 4)")
-    p.add_argument("--ess-draws", type=int, default=100,
-                   help="post-warmup draws per chain for the ESS / accuracy phase (after the timed steps)")
+    p.add_argument("--ess-draws", type=int, default=250,
+                   help="post-warmup draws per chain for the ESS / accuracy phase (after the timed steps); "
+                        "ESS/s counts the warmup too, so it rises with the draws per warmup iteration "
+                        "(Stan's defaults: 1000 and 1000)")
     p.add_argument("--no-accuracy", action="store_true", help="skip the full-data Laplace reference")
     p.add_argument("--nuts-criterion", choices=["stan2.19", "stan2.23"], default="stan2.23",
                    help="stan2.23 (default): Stan's NUTS with the U-turn checks across subtree junctions "

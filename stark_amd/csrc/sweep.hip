@@ -1865,16 +1865,9 @@ constexpr int G5_NS = 4;
 // A barrier that leaves LDS-DMAs in flight: __syncthreads() makes hipcc drain vmcnt(0) first
 // (an LDS-DMA is a pending LDS write on the VM counter), which would empty the stage ring at
 // every stage; the counted wait before it is what orders the DMA'd data.
-#ifndef G5_RAWBAR
-#define G5_RAWBAR 1
-#endif
 __device__ __forceinline__ void lds_barrier() {
-  if constexpr (G5_RAWBAR) {
-    __builtin_amdgcn_s_waitcnt(0xC07F);                 // lgkmcnt(0): this wave's LDS accesses done
-    __builtin_amdgcn_s_barrier();
-  } else {
-    __syncthreads();
-  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);                   // lgkmcnt(0): this wave's LDS accesses done
+  __builtin_amdgcn_s_barrier();
 }
 constexpr int G5_DMA = 4;     // DMA instructions per wave per stage (2 for each operand image)
 #ifndef G5_FW
