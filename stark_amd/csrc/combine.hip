@@ -33,7 +33,7 @@ namespace stk {
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
-// ---- tile loaders: a(m, k), b(k, n), store(m, n, v)
+// ---- tile loaders: a4(m, k..k+3), b4(k..k+3, n) (zero past K; k % 4 == 0), store(m, n, v)
 struct CovLd {               // batch = shard (blockIdx.z)
   const double* X;           // [shard][P][S]
   const double* mean;        // [shard][P]
@@ -41,11 +41,26 @@ struct CovLd {               // batch = shard (blockIdx.z)
   double* cov;               // [shard][P][P]
   int P, S;
   double scale;
-  __device__ double a(int z, int m, int k) const { return X[((size_t)z * P + m) * S + k] - mean[(size_t)z * P + m]; }
-  __device__ double b(int z, int k, int n) const { return X[((size_t)z * P + n) * S + k] - mean[(size_t)z * P + n]; }
   __device__ void store(int z, int m, int n, double v) const {
     cov[((size_t)z * P + m) * P + n] = (blk && blk[m] != blk[n]) ? 0.0 : v * scale;
   }
+  // 4 consecutive k of one centred row (k % 4 == 0): two 16-B loads when the row is 16-B aligned
+  __device__ void row4(int z, int m, int k, int K, double* v) const {
+    const double* row = X + ((size_t)z * P + m) * S;
+    const double mu = mean[(size_t)z * P + m];
+    if (k + 3 < K && !(S & 1)) {
+      const dbl2 x0 = *reinterpret_cast<const dbl2*>(row + k), x1 = *reinterpret_cast<const dbl2*>(row + k + 2);
+      v[0] = x0.x - mu;
+      v[1] = x0.y - mu;
+      v[2] = x1.x - mu;
+      v[3] = x1.y - mu;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = k + j < K ? row[k + j] - mu : 0.0;
+    }
+  }
+  __device__ void a4(int z, int m, int k, int K, double* v) const { row4(z, m, k, K, v); }
+  __device__ void b4(int z, int k, int n, int K, double* v) const { row4(z, n, k, K, v); }
 };
 struct WThetaLd {            // sum_s W_s theta_s, K = nshards * P
   const double* W;           // [shard][P][P]
@@ -53,21 +68,49 @@ struct WThetaLd {            // sum_s W_s theta_s, K = nshards * P
   const int32_t* used;       // [shard]
   double* out;               // [P][S]
   int P, S;
-  __device__ double a(int, int m, int k) const {
-    const int s = k / P;
-    return used[s] ? W[((size_t)s * P + m) * P + (k - s * P)] : 0.0;
-  }
-  __device__ double b(int, int k, int n) const { return used[k / P] ? X[(size_t)k * S + n] : 0.0; }
   __device__ void store(int, int m, int n, double v) const { out[(size_t)m * S + n] = v; }
+  // k % 4 == 0; the shards of k .. k+3 follow from k's with one division per call.
+  // W of a NaN shard is 0 already (k_spd_inverse), its draws are masked here
+  __device__ void a4(int, int m, int k, int K, double* v) const {
+    int sh = k / P, r = k - sh * P;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = k + j < K ? W[((size_t)sh * P + m) * P + r] : 0.0;
+      if (++r == P) { r = 0; ++sh; }
+    }
+  }
+  __device__ void b4(int, int k, int n, int K, double* v) const {
+    int sh = k / P, r = k - sh * P;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = (k + j < K && used[sh]) ? X[(size_t)(k + j) * S + n] : 0.0;
+      if (++r == P) { r = 0; ++sh; }
+    }
+  }
 };
 struct PlainLd {             // C[M x N] = A[M x K] . B[K x N], row-major
   const double* A;
   const double* B;
   double* C;
   int lda, ldb, ldc;
-  __device__ double a(int, int m, int k) const { return A[(size_t)m * lda + k]; }
-  __device__ double b(int, int k, int n) const { return B[(size_t)k * ldb + n]; }
   __device__ void store(int, int m, int n, double v) const { C[(size_t)m * ldc + n] = v; }
+  __device__ void a4(int, int m, int k, int K, double* v) const {
+    const double* row = A + (size_t)m * lda;
+    if (k + 3 < K && !(lda & 1)) {
+      const dbl2 x0 = *reinterpret_cast<const dbl2*>(row + k), x1 = *reinterpret_cast<const dbl2*>(row + k + 2);
+      v[0] = x0.x;
+      v[1] = x0.y;
+      v[2] = x1.x;
+      v[3] = x1.y;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = k + j < K ? row[k + j] : 0.0;
+    }
+  }
+  __device__ void b4(int, int k, int n, int K, double* v) const {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = k + j < K ? B[(size_t)(k + j) * ldb + n] : 0.0;
+  }
 };
 
 // fp64 MFMA GEMM for the combine's products (v_mfma_f64_16x16x4_f64).  One block = MG_KW waves
@@ -117,13 +160,21 @@ __global__ __launch_bounds__(64 * MG_KW) void k_mgemm(LD L, int M, int N, int K,
     for (int h = 0; h < CH; ++h) {
       const int k = 16 * (c0 + h) + 4 * g;
       const bool live = c0 + h < ge;
+      if (live && ma < M) {
+        L.a4(z, ma, k, K, a[h]);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) a[h][j] = (live && ma < M && k + j < K) ? L.a(z, ma, k + j) : 0.0;
+        for (int j = 0; j < 4; ++j) a[h][j] = 0.0;
+      }
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         const int n = n0 + 16 * nb + r;
+        if (live && n < N) {
+          L.b4(z, k, n, K, b[h][nb]);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b[h][nb][j] = (live && n < N && k + j < K) ? L.b(z, k + j, n) : 0.0;
+          for (int j = 0; j < 4; ++j) b[h][nb][j] = 0.0;
+        }
       }
     }
 #pragma unroll

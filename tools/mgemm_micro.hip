@@ -9,16 +9,22 @@
 struct SynthLd {             // operands from arithmetic only (no loads)
   double* out;
   int P;
-  __device__ double a(int z, int m, int k) const { return 1e-3 * (m + 1) + 1e-6 * (k & 63) + z; }
-  __device__ double b(int z, int k, int n) const { return 1e-3 * (n + 1) - 1e-6 * (k & 31) + z; }
+  __device__ void a4(int z, int m, int k, int, double* v) const {
+    for (int j = 0; j < 4; ++j) v[j] = 1e-3 * (m + 1) + 1e-6 * ((k + j) & 63) + z;
+  }
+  __device__ void b4(int z, int k, int n, int, double* v) const {
+    for (int j = 0; j < 4; ++j) v[j] = 1e-3 * (n + 1) - 1e-6 * ((k + j) & 31) + z;
+  }
   __device__ void store(int z, int m, int n, double v) const { out[((size_t)z * P + m) * P + n] = v; }
 };
 struct RowLd {               // Cov shape from plain row-major pointers, no centring
   const double* X;
   double* out;
   int P, S;
-  __device__ double a(int z, int m, int k) const { return X[((size_t)z * P + m) * S + k]; }
-  __device__ double b(int z, int k, int n) const { return X[((size_t)z * P + n) * S + k]; }
+  __device__ void a4(int z, int m, int k, int K, double* v) const {
+    for (int j = 0; j < 4; ++j) v[j] = k + j < K ? X[((size_t)z * P + m) * S + k + j] : 0.0;
+  }
+  __device__ void b4(int z, int k, int n, int K, double* v) const { a4(z, n, k, K, v); }
   __device__ void store(int z, int m, int n, double v) const { out[((size_t)z * P + m) * P + n] = v; }
 };
 
