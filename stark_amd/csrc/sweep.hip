@@ -987,9 +987,15 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
 #ifndef SE_NACC
 #define SE_NACC 2             // forward accumulators (4: same time, more registers; 8: spills)
 #endif
+// beta image row stride = 4 KF + SE_BPAD doubles: at 100 doubles (200 dwords = 8 mod 64 banks)
+// chains c and c + 8 of one 32-lane group hit the same banks (2-way); 102 spreads the 16 chains
+// of a group over 16 distinct bank pairs, lane groups lh = 0 / 1 on the other parity
+#ifndef SE_BPAD
+#define SE_BPAD 2
+#endif
 template <int FAM, int KF, int JT, int ABL = 0>
 __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
-  constexpr int C = SM_C, NW = SM_W, JTV = JT - 1, KP = 4 * KF;
+  constexpr int C = SM_C, NW = SM_W, JTV = JT - 1, KP = 4 * KF, KB = KP + SE_BPAD;
   const int shard = A.shard0 + blockIdx.x / A.G;
   const int chunk = blockIdx.x % A.G;
   if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
@@ -1010,13 +1016,13 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
 
   extern __shared__ __attribute__((aligned(16))) double lds[];
   char* const slot = reinterpret_cast<char*>(lds) + (size_t)w * SS;
-  double* const bimg = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);  // [16][KP]
-  double* const sptab = bimg + C * KP;
+  double* const bimg = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);  // [16][KB]
+  double* const sptab = bimg + C * KB;
   if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
   const double* qs = A.q + (size_t)shard * C * A.Dp;
   for (int i = tid; i < C * KP; i += NW * 64) {
     const int c = i / KP, col = i % KP;
-    bimg[i] = col < d ? qs[(size_t)c * A.Dp + 1 + col] : 0.0;
+    bimg[c * KB + col] = col < d ? qs[(size_t)c * A.Dp + 1 + col] : 0.0;
   }
   const double alpha = qs[(size_t)lr * A.Dp];
   const double inv_s = (FAM == STK_LINREG) ? exp(-qs[(size_t)lr * A.Dp + d + 1]) : 0.0;
@@ -1046,7 +1052,7 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   double gv[4] = {0.0, 0.0, 0.0, 0.0};
   double lpa = 0.0, gaa = 0.0;
   const double* xs = reinterpret_cast<const double*>(slot);
-  const double* brow = bimg + lr * KP + lh * KF;
+  const double* brow = bimg + lr * KB + lh * KF;
 
   if (mine > 0) issue(0);
   for (int k = 0; k < mine; ++k) {
@@ -2303,7 +2309,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     }
     const int JT = (d + 15) / 16;
     size_t ring = (size_t)SM_W * nb * sweepm_slot_bytes(d) + SP_TAB * sizeof(double);
-    if (d == 100) ring = (size_t)SM_W * sweepm_slot_bytes(d) + (16 * 100 + SP_TAB) * sizeof(double);   // v4e
+    if (d == 100) ring = (size_t)SM_W * sweepm_slot_bytes(d) + (16 * (100 + SE_BPAD) + SP_TAB) * sizeof(double);   // v4e
     const size_t red = ((size_t)SM_W * JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * sizeof(double);
     *lds_bytes = std::max(ring, red);
     return;

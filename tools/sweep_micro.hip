@@ -266,7 +266,7 @@ int main(int argc, char** argv) {
     };
     abl("v4 generic", k_sweepm<STK_LOGREG, 0, 0, 0>);
     {
-      const size_t le = std::max((size_t)SM_W * sweepm_slot_bytes(d) + 16 * 100 * 8 + SP_TAB * 8, lds);
+      const size_t le = std::max((size_t)SM_W * sweepm_slot_bytes(d) + 16 * (100 + SE_BPAD) * 8 + SP_TAB * 8, lds);
       auto ke = [&](const char* name, auto kern) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         timeit(name, bytes, [&] { hipLaunchKernelGGL(kern, dim3(nsh * G), dim3(256), le, st, A4); });
