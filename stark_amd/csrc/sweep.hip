@@ -708,7 +708,7 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 constexpr int SM_W = 4;                 // waves per block (one per SIMD)
 constexpr int SM_R = 16;                // rows per wave sub-tile = MFMA M (forward) and K (backward)
 constexpr int SM_C = 16;                // chains per launch row = MFMA N
-constexpr int SM_MINB = 2;              // blocks per CU: two waves per SIMD (fp64 MFMA issue from one wave tops out at ~75 %)
+constexpr int SM_MINB = 2;              // blocks per CU: two waves per SIMD (one wave cannot cover the slot's DMA latency)
 __host__ __device__ constexpr int sweepm_slot_bytes(int d) { return SM_R * d * 8 + 128; }
 
 __device__ __forceinline__ dbl4 mfma_f64(double a, double b, dbl4 c) {
@@ -1413,8 +1413,9 @@ __global__ __launch_bounds__(256, 2) void k_sweepr(SweepArgs A) {
 // v6 (k_sweepq): the 16-chain sweep on the four-block fp64 MFMA, v_mfma_f64_4x4x4_4b_f64.
 //
 // On gfx950 the four-block 4x4x4 form issues every 16.5 cycles per SIMD (512 flop: 75 TF/s
-// chip-wide, 96 % of the 78.6 TF spec) where v_mfma_f64_16x16x4_f64 issues every 105 (2048
-// flop: 47.9 TF/s) -- profiles/r02n_mfma4.log, r02b_mfma_ceiling.log.  Lane layout (measured,
+// chip-wide), the same rate per flop as v_mfma_f64_16x16x4_f64 (64 cycles, 2048 flop, 78 TF/s;
+// profiles/r02zd_mfma_ceiling_vgprform.log -- an earlier reading of 105 cycles was a
+// micro-benchmark codegen artefact).  Lane layout (measured,
 // tools/mfma4_layout.hip): A lane = m + 4 blk + 16 k, B lane = n + 4 blk + 16 k, D lane =
 // n + 4 blk + 16 m.  The four blocks are the four groups of 4 chains, so with lr = lane & 15
 // (chain) and lh = lane >> 4 every operand is one f64 per lane and nothing is shuffled:
