@@ -227,10 +227,12 @@ def main():
     i0 = sampler.info()
     barrier()
     t0 = time.perf_counter()
+    w0 = time.monotonic_ns()
     sampler.run(A + n_samp, max_steps=K)
     ctx.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    w1 = time.monotonic_ns()
     ctx.set_profiling(False)
     i1 = sampler.info()
     it1 = sampler.iterations()
@@ -493,6 +495,7 @@ def main():
                     "note": "engine.consensus(separate_lp=True) on host buffers: host->device copy of the draws, "
                             "the combine kernels, the result copied back"},
         "setup_s": {"datagen": t_gen, "adaptation": t_adapt, "post_warmup_draws": t_post},
+        "timed_window_monotonic_ns": [w0, w1],     # tools/rocpd_summary.py window: the kernel trace's dispatches in it
         "divergent": info["divergent"],
     }
     print(json.dumps(line), flush=True)

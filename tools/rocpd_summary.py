@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Summaries of rocprofv3 rocpd (.db, SQLite) outputs, for profiles/:
   stats  <db> [--csv out]                 per-kernel call count / total / average duration (us)
+  window <db> --kernel K --bench-json J   average duration of kernel K's dispatches inside the
+                                          bench line's timed window (timed_window_monotonic_ns;
+                                          rocprofv3 stamps dispatches on the same monotonic clock):
+                                          the figure bench.py's roofline.avg_launch_ms must match
   pmc    <db> --kernel K [--json out]     per-dispatch counter values of kernel K (summed over
                                           the rows of a dispatch), their median, and the derived
                                           figures: fp64 MFMA flops (MOPS_F64 x 512), MFMA busy % of
@@ -14,7 +18,8 @@ import sqlite3
 import statistics
 
 p = argparse.ArgumentParser()
-p.add_argument("mode", choices=["stats", "pmc"])
+p.add_argument("mode", choices=["stats", "pmc", "window"])
+p.add_argument("--bench-json")
 p.add_argument("db")
 p.add_argument("--kernel", default="k_sweepm")
 p.add_argument("--csv")
@@ -28,7 +33,19 @@ p.add_argument("--shards-per-gpu", type=int)
 a = p.parse_args()
 cur = sqlite3.connect(a.db).cursor()
 
-if a.mode == "stats":
+if a.mode == "window":
+    line = json.loads(open(a.bench_json).read().strip().splitlines()[-1])
+    w0, w1 = line["timed_window_monotonic_ns"]
+    rows = list(cur.execute("select start, end from kernels where name like ? order by start", (f"%{a.kernel}%",)))
+    inside = [(e - s_) * 1e-6 for s_, e in rows if s_ >= w0 and e <= w1]
+    out = {"kernel": a.kernel, "dispatches_total": len(rows), "window_dispatches": len(inside),
+           "bench_steps": line["steps"], "window_avg_ms": statistics.mean(inside) if inside else None,
+           "window_median_ms": statistics.median(inside) if inside else None,
+           "bench_avg_launch_ms": line["roofline"]["avg_launch_ms"]}
+    print(json.dumps(out))
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+elif a.mode == "stats":
     rows = list(cur.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
     # top_kernels durations are in microseconds
     lines = ["kernel,calls,total_ms,avg_ms,percent"] + [
