@@ -246,3 +246,32 @@ def test_prior_lpgrad(ctx, orc, family, C):
     np.testing.assert_array_equal(g0, g1)
     m.close()
     flat.close()
+
+
+# ---------------------------------------------------------------- the headline shapes at full size
+def test_fullsize_shards_sum_to_full_data(ctx):
+    """BASELINE configs[3] at full size (N = 1e8, d = 100, 16 chains: the k_sweepe launch of the
+    bench): the log density of a flat-prior logistic regression is a sum over rows, so the 8
+    subposterior shards' lp and gradient must add up to those of ONE shard holding all 1e8 rows
+    (the same Philox rows, generated by global row index).  The two sums run over different chunk
+    structures, so they agree to rounding: 1e-12 relative on lp, the sweep tolerance on the
+    gradient.  Size-independent property; the oracle covers the arithmetic at small n."""
+    from stark_amd import engine
+    n, S, d, C, seed = 100_000_000, 8, 100, 16, 20240
+    truth = np.concatenate([[0.0], engine.Model.gen_beta(seed, d)])
+    q = truth + np.random.default_rng(3).normal(0, 2e-3, (C, d + 1))
+    m8 = engine.Model.synthetic(ctx, "logistic", S, n // S, d, data_seed=seed)
+    lp8, g8 = np.zeros(C), np.zeros((C, d + 1))
+    for s in range(S):
+        lp, g = m8.log_density_grad(s, q)
+        lp8 += lp
+        g8 += g
+    m8.close()
+    m1 = engine.Model.synthetic(ctx, "logistic", 1, n, d, data_seed=seed)
+    lp1, g1 = m1.log_density_grad(0, q)
+    m1.close()
+    assert np.all(np.abs(lp8 - lp1) <= 1e-12 * np.abs(lp1)), np.abs(lp8 - lp1) / np.abs(lp1)
+    for c in range(C):
+        scale = np.abs(g1[c]).max() + 1.0
+        assert np.all(np.abs(g8[c] - g1[c]) <= RTOL_LP * np.maximum(np.abs(g1[c]), scale * 1e-3)), \
+            (c, np.abs(g8[c] - g1[c]).max(), scale)
