@@ -1878,9 +1878,15 @@ __device__ __forceinline__ void lds_barrier() {
 }
 constexpr int G5_DMA = 4;     // DMA instructions per wave per stage (2 for each operand image)
 #ifndef G5_FW
-#define G5_FW 4               // pass F: waves per block (4: two blocks per CU, NS = 2)
-#define G5_FS 2
+#define G5_FW 4               // pass F: waves per block (4: two blocks per CU)
 #endif
+#ifndef G5_FS
+#define G5_FS 2               // pass F: stages in the ring
+#endif
+#ifndef G5_FKC
+#define G5_FKC 32             // pass F: columns per stage (32: 32 KB stages; 16: 16 KB)
+#endif
+__host__ __device__ constexpr int g5_fstage_bytes() { return 1024 * G5_FKC; }
 
 // Pass F: one block per (shard, chunk); the chunk's 64-row tiles one after another.  NW waves
 // (4: two blocks per CU, a double buffer; 8: one block per CU, the 4-stage ring), each with
@@ -1889,13 +1895,21 @@ constexpr int G5_DMA = 4;     // DMA instructions per wave per stage (2 for each
 // the other's GEMM, which measured faster for this pass.
 template <int FAM>
 __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A) {
-  constexpr int NW = G5_FW, NS = G5_FS, NCT = 16 / NW, NDMA = 16 / NW;
+  constexpr int NW = G5_FW, NS = G5_FS, NCT = 16 / NW;
+  constexpr int KCF = G5_FKC, STG = g5_fstage_bytes(), XB = STG / 2;   // stage: [X 64 x KCF][beta^T KCF x 64]
+  constexpr int PPR = KCF / 2;                          // 16-B pieces per X row in the stage
+  constexpr int NDMA = (XB / 1024) / NW;                // DMA instructions per wave per operand image
+  constexpr int EV = STG / NW / 512;                    // eta values per wave per epilogue round
+  static_assert(NDMA >= 1 && EV >= 1 && (4 * NCT) % EV == 0, "pass F stage geometry");
+  // X piece swizzle: 256-B rows (PPR 16) XOR the piece with row & 15; 128-B rows (PPR 8) put
+  // rows of one parity on one half of the banks, so XOR with (row >> 1) & 7
+  auto swz = [](int row) { return PPR == 16 ? (row & 15) : ((row >> 1) & 7); };
   const int shard = A.shard0 + blockIdx.x / A.G;
   const int chunk = blockIdx.x % A.G;
   if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
   if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
   const ShardDev sh = A.shards[shard];
-  const int d = sh.d, KP = g5_kp(d), NKC = KP / G5_KC;
+  const int d = sh.d, KP = g5_kp(d), NKC = KP / KCF;
   const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
   const int wr = w & 3, wc = w >> 2;
   const int lr = lane & 15, lh = lane >> 4;
@@ -1906,8 +1920,8 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
   const int ntile = (int)(t1 - t0);
 
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  char* const stg = reinterpret_cast<char*>(lds);                 // NS stages: [X 16 KB][beta^T 16 KB]
-  double* const sptab = reinterpret_cast<double*>(stg + NS * G5_STAGE);
+  char* const stg = reinterpret_cast<char*>(lds);                 // NS stages of STG bytes
+  double* const sptab = reinterpret_cast<double*>(stg + NS * STG);
   if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
 
   // per-lane chain constants: chain 16 ct + lr, ct = 2 wc + c2
@@ -1924,24 +1938,24 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
 
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
   const __amdgpu_buffer_rsrc_t br = uniform_rsrc(A.qT + (size_t)shard * KP * G5_C, (int64_t)KP * G5_C * 8);
-  // X stage: slot s (16 B) = row s>>4, piece (s & 15) ^ (row & 15) of the stage's 32 columns
+  // X stage: slot s (16 B) = row s / PPR, piece (s % PPR) ^ swz(row) of the stage's KCF columns
   int xvo[NDMA];
 #pragma unroll
   for (int i = 0; i < NDMA; ++i) {
-    const int sl = (w * NDMA + i) * 64 + lane, row = sl >> 4, pc = (sl & 15) ^ (row & 15);
+    const int sl = (w * NDMA + i) * 64 + lane, row = sl / PPR, pc = (sl % PPR) ^ swz(row);
     xvo[i] = row * d * 8 + pc * 16;
   }
   auto issue = [&](int st) {          // global stage index st = tile * NKC + kc
     const int tile = st / NKC, kc = st % NKC;
-    char* b = stg + (st % NS) * G5_STAGE;
-    const int xso = tile * G5_TR * d * 8 + kc * G5_KC * 8;
+    char* b = stg + (st % NS) * STG;
+    const int xso = tile * G5_TR * d * 8 + kc * KCF * 8;
 #pragma unroll
     for (int i = 0; i < NDMA; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * NDMA + i) * 1024), 16, xvo[i], xso, 0, 0);
 #pragma unroll
     for (int i = 0; i < NDMA; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(br, (lds_vptr)(b + 16384 + (w * NDMA + i) * 1024), 16, lane * 16,
-                                               kc * G5_KC * 512 + (w * NDMA + i) * 1024, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(br, (lds_vptr)(b + XB + (w * NDMA + i) * 1024), 16, lane * 16,
+                                               kc * KCF * 512 + (w * NDMA + i) * 1024, 0, 0);
   };
 
   double lpa[NCT], gaa[NCT];
@@ -1969,64 +1983,65 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
         yt[i] = grow < nrows ? ((FAM == STK_LOGREG) ? (double)sh.yi[r0 + grow] : sh.y[r0 + grow]) : 0.0;
       }
     }
-    const char* b = stg + (st % NS) * G5_STAGE;
+    const char* b = stg + (st % NS) * STG;
     const int r = 16 * wr + lr;
 #pragma unroll
-    for (int step = 0; step < G5_KC / 4; ++step) {
+    for (int step = 0; step < KCF / 4; ++step) {
       const int kk = 4 * step + lh;
-      const double a = *reinterpret_cast<const double*>(b + r * 256 + ((((kk >> 1) ^ (r & 15))) << 4) + ((kk & 1) << 3));
+      const double a = *reinterpret_cast<const double*>(b + r * (16 * PPR) + (((kk >> 1) ^ swz(r)) << 4) + ((kk & 1) << 3));
 #pragma unroll
       for (int c2 = 0; c2 < NCT; ++c2)
-        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + 16384 + g5_chain_off(kk, 16 * (NCT * wc + c2) + lr)), acc[c2]);
+        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + XB + g5_chain_off(kk, 16 * (NCT * wc + c2) + lr)), acc[c2]);
     }
     if (kc == NKC - 1) {                                 // ---- tile epilogue: residual, R, lp
       lds_barrier();                                     // every wave is done reading stage st
-      // eta goes through this wave's own 2 NCT KB of the stage just consumed (refilled only
-      // after the next barrier), so the residuals run one at a time from LDS instead of holding
-      // 4 NCT softplus evaluations' temporaries in registers
+      // eta goes through this wave's own STG / NW bytes of the stage just consumed (refilled
+      // only after the next barrier), EV values per round, so the residuals run one at a time
+      // from LDS instead of holding 4 NCT softplus evaluations' temporaries in registers
       const int tile = st / NKC;
-      char* const b2 = stg + (st % NS) * G5_STAGE;
-      auto eslot = [&](int e) -> double* { return reinterpret_cast<double*>(b2 + w * (NCT * 2048) + e * 512) + lane; };
+      char* const b2 = stg + (st % NS) * STG;
+      auto eslot = [&](int e) -> double* { return reinterpret_cast<double*>(b2 + w * (EV * 512) + (e % EV) * 512) + lane; };
 #pragma unroll
-      for (int c2 = 0; c2 < NCT; ++c2)
+      for (int e0 = 0; e0 < 4 * NCT; e0 += EV) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) *eslot(c2 * 4 + i) = acc[c2][i];
+        for (int e = e0; e < e0 + EV; ++e) *eslot(e) = acc[e >> 2][e & 3];
 #pragma unroll 1
-      for (int e = 0; e < 4 * NCT; ++e) {
-        const int c2 = e >> 2, i = e & 3, ct = NCT * wc + c2;
-        const int row = 16 * wr + lh + 4 * i;              // row of the tile
-        const int64_t grow = (int64_t)tile * G5_TR + row;  // row of the chunk
-        const bool valid = grow < nrows;
-        const double yv = i == 0 ? yt[0] : (i == 1 ? yt[1] : (i == 2 ? yt[2] : yt[3]));
-        double al = alpha[0], isg = inv_s[0];
+        for (int e = e0; e < e0 + EV; ++e) {
+          const int c2 = e >> 2, i = e & 3, ct = NCT * wc + c2;
+          const int row = 16 * wr + lh + 4 * i;              // row of the tile
+          const int64_t grow = (int64_t)tile * G5_TR + row;  // row of the chunk
+          const bool valid = grow < nrows;
+          const double yv = i == 0 ? yt[0] : (i == 1 ? yt[1] : (i == 2 ? yt[2] : yt[3]));
+          double al = alpha[0], isg = inv_s[0];
 #pragma unroll
-        for (int q = 1; q < NCT; ++q)
-          if (c2 == q) {
-            al = alpha[q];
-            isg = inv_s[q];
+          for (int q = 1; q < NCT; ++q)
+            if (c2 == q) {
+              al = alpha[q];
+              isg = inv_s[q];
+            }
+          const double eta = *eslot(e) + al;
+          double dv, lt;
+          if constexpr (FAM == STK_LOGREG) {
+            const double sgn = 2.0 * yv - 1.0, ntt = sgn * eta;
+            double ex, lm, wt;
+            softplus_tab(ntt, sptab, &ex, &lm, &wt);
+            const bool hi = ntt > 20.0, lo = ntt < -20.0;
+            lt = hi ? -ex : (lo ? ntt : -lm);
+            dv = sgn * (hi ? ex : (lo ? 1.0 : wt));
+          } else {
+            const double z = (yv - eta) * isg;
+            lt = z * z;
+            dv = z * isg;
           }
-        const double eta = *eslot(e) + al;
-        double dv, lt;
-        if constexpr (FAM == STK_LOGREG) {
-          const double sgn = 2.0 * yv - 1.0, ntt = sgn * eta;
-          double ex, lm, wt;
-          softplus_tab(ntt, sptab, &ex, &lm, &wt);
-          const bool hi = ntt > 20.0, lo = ntt < -20.0;
-          lt = hi ? -ex : (lo ? ntt : -lm);
-          dv = sgn * (hi ? ex : (lo ? 1.0 : wt));
-        } else {
-          const double z = (yv - eta) * isg;
-          lt = z * z;
-          dv = z * isg;
-        }
-        dv = valid ? dv : 0.0;
-        lt = valid ? lt : 0.0;
+          dv = valid ? dv : 0.0;
+          lt = valid ? lt : 0.0;
 #pragma unroll
-        for (int q = 0; q < NCT; ++q) {
-          lpa[q] += q == c2 ? lt : 0.0;
-          gaa[q] += q == c2 ? dv : 0.0;
+          for (int q = 0; q < NCT; ++q) {
+            lpa[q] += q == c2 ? lt : 0.0;
+            gaa[q] += q == c2 ? dv : 0.0;
+          }
+          *reinterpret_cast<double*>(Rimg + g5_chain_off((int)grow, 16 * ct + lr)) = dv;
         }
-        *reinterpret_cast<double*>(Rimg + g5_chain_off((int)grow, 16 * ct + lr)) = dv;
       }
       __builtin_amdgcn_s_waitcnt(0xF70);                  // vmcnt(0): R stores retired before the next counted DMA wait
     }
@@ -2284,7 +2299,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *T = G5_TR;
     *LD = 0;
     *G = (int)g;
-    *lds_bytes = G5_FS * G5_STAGE + SP_TAB * sizeof(double);
+    *lds_bytes = G5_FS * g5_fstage_bytes() + SP_TAB * sizeof(double);
     return;
   }
   if (var == 4) {
