@@ -263,3 +263,31 @@ def test_laplace_reference_matches_closed_form_gaussian():
     m, c, info = L.laplace(Quad(), [0, 1], mu + 0.3, np.ones(D))
     np.testing.assert_allclose(m, mu, rtol=0, atol=1e-9)
     np.testing.assert_allclose(c, np.linalg.inv(prec), rtol=1e-7, atol=1e-10)
+
+
+def test_rocpd_window_selects_the_timed_dispatches(tmp_path):
+    """tools/rocpd_summary.py window: the kernel dispatches inside the bench line's timed window
+    (timed_window_monotonic_ns) and nothing else -- the figure the line's roofline.avg_launch_ms
+    is checked against."""
+    import json
+    import sqlite3
+    import subprocess
+    import sys
+    db = tmp_path / "run_results.db"
+    con = sqlite3.connect(db)
+    con.execute("create table kernels (name text, start integer, end integer)")
+    rows = [("void stk::k_sweepe<3, 25, 7, 0>(stk::SweepArgs)", t, t + d) for t, d in
+            [(100, 5_000_000), (20_000_000, 17_000_000), (40_000_000, 17_200_000), (60_000_000, 16_800_000),
+             (90_000_000, 9_000_000)]] + [("stk::k_nuts_step", 38_000_000, 38_100_000)]
+    con.executemany("insert into kernels values (?, ?, ?)", rows)
+    con.commit()
+    con.close()
+    line = tmp_path / "bench.json"
+    line.write_text(json.dumps({"timed_window_monotonic_ns": [19_000_000, 80_000_000], "steps": 3,
+                                "roofline": {"avg_launch_ms": 17.0}}) + "\n")
+    out = subprocess.run([sys.executable, "tools/rocpd_summary.py", "window", str(db), "--kernel", "k_sweepe",
+                          "--bench-json", str(line)], capture_output=True, text=True, check=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["window_dispatches"] == 3 and rec["dispatches_total"] == 5
+    assert abs(rec["window_avg_ms"] - 17.0) < 1e-9
