@@ -1840,7 +1840,6 @@ static size_t sweepq_lds(int S, int NB, int KF, int d) {
 constexpr int G5_C = 64;      // chains (4 MFMA N tiles)
 constexpr int G5_KC = 32;     // pass F: columns per stage
 constexpr int G5_TR = 64;     // pass F: rows per tile (16 per wave)
-constexpr int G5_JB = 64;     // pass B: columns per block (16 per wave)
 constexpr int G5_RB = 32;     // pass B: rows per stage
 constexpr int G5_STAGE = 32 * 1024;   // bytes per stage (A image + B image)
 
@@ -2065,15 +2064,29 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
   }
 }
 
-// Pass B: one block per (shard, chunk, 64-column block); G[j][c] += X[r][j] R[r][c] over the
-// chunk's rows, straight into the chunk's partial row (columns 1 .. d).
+// Pass B: one block per (shard, chunk, JB-column block); G[j][c] += X[r][j] R[r][c] over the
+// chunk's rows, straight into the chunk's partial row (columns 1 .. d).  8 waves: wave w takes
+// column group w % WC (16 columns) and chain group w / WC (NCT 16-chain MFMA tiles); JB = 128
+// (default): 8 column groups x all 64 chains (4 MFMAs per A read), 48 KB stages in a 3-deep ring;
+// JB = 64: 4 column groups x 2 chain halves, 32 KB stages in a 4-deep ring (4 % slower).
+#ifndef G5_BJB
+#define G5_BJB 128
+#endif
+#ifndef G5_BNS
+#define G5_BNS 3
+#endif
+__host__ __device__ constexpr int g5_bstage_bytes() { return 32 * G5_BJB * 8 + 16384; }
 __global__ __launch_bounds__(64 * G5_NW, 1) void k_gemm_bwd(SweepArgs A, int njb) {
+  constexpr int JB = G5_BJB, NSB = G5_BNS, WC = JB / 16, NCT = 4 * WC / G5_NW;
+  constexpr int XB = G5_RB * JB * 8, STG = g5_bstage_bytes(), PPR = JB / 2;
+  constexpr int NDX = XB / 1024 / G5_NW, NDR = 16384 / 1024 / G5_NW;   // DMA instructions per wave
+  static_assert(NDX >= 1 && NDR >= 1 && NCT >= 1 && STG == XB + 16384, "pass B stage geometry");
   // XCD-aware order: blocks are dealt to the 8 XCDs round-robin (blockIdx % 8), so the njb
   // column blocks of a chunk get blockIdx values of one residue -- one XCD, whose L2 then
   // serves the chunk's R rows to all of them (else each XCD re-reads R from HBM)
-  const int NS = gridDim.x / njb;
+  const int nsc = gridDim.x / njb;
   int sc, jb;
-  if ((NS & 7) == 0) {
+  if ((nsc & 7) == 0) {
     const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
     sc = x + 8 * (k / njb);
     jb = k % njb;
@@ -2087,61 +2100,64 @@ __global__ __launch_bounds__(64 * G5_NW, 1) void k_gemm_bwd(SweepArgs A, int njb
   const ShardDev sh = A.shards[shard];
   const int d = sh.d;
   const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
-  const int wr = w & 3, wc = w >> 2;
+  const int cw = w % WC, cg = w / WC;
   const int lr = lane & 15, lh = lane >> 4;
   const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;
   const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
   const int64_t r0 = t0 * G5_TR, r1 = std::min<int64_t>(sh.n, t1 * G5_TR);
   const int nrows = (int)(r1 - r0);
   const int nst = (nrows + G5_RB - 1) / G5_RB;
-  const int j0 = jb * G5_JB;
+  const int j0 = jb * JB;
 
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  char* const stg = reinterpret_cast<char*>(lds);      // G5_NS stages: [X^T block 16 KB][R block 16 KB]
+  char* const stg = reinterpret_cast<char*>(lds);      // NSB stages: [X^T block XB][R block 16 KB]
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
   const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(A.R + ((size_t)shard * A.Rrows + r0) * G5_C, (int64_t)nrows * G5_C * 8);
-  // X stage: slot s = row s >> 5, piece (s & 31) ^ ((row & 1) << 3) of the block's 64 columns
-  int xvo[2];
+  // X stage: slot s = row s / PPR, piece (s % PPR) ^ ((row & 1) << 3) of the block's JB columns
+  // (rows 4s + lh of one lane group then sit on opposite halves of the banks)
+  int xvo[NDX];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int sl = (w * 2 + i) * 64 + lane, row = sl >> 5, pc = (sl & 31) ^ ((row & 1) << 3);
+  for (int i = 0; i < NDX; ++i) {
+    const int sl = (w * NDX + i) * 64 + lane, row = sl / PPR, pc = (sl % PPR) ^ ((row & 1) << 3);
     xvo[i] = row * d * 8 + (j0 + 2 * pc) * 8;
   }
   auto issue = [&](int st) {
-    char* b = stg + (st % G5_NS) * G5_STAGE;
+    char* b = stg + (st % NSB) * STG;
     const int xso = st * G5_RB * d * 8;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * 2 + i) * 1024), 16, xvo[i], xso, 0, 0);
+    for (int i = 0; i < NDX; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * NDX + i) * 1024), 16, xvo[i], xso, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (lds_vptr)(b + 16384 + (w * 2 + i) * 1024), 16, lane * 16,
-                                               st * G5_RB * 512 + (w * 2 + i) * 1024, 0, 0);
+    for (int i = 0; i < NDR; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (lds_vptr)(b + XB + (w * NDR + i) * 1024), 16, lane * 16,
+                                               st * G5_RB * 512 + (w * NDR + i) * 1024, 0, 0);
   };
-  dbl4 acc[2] = {dbl4{0.0, 0.0, 0.0, 0.0}, dbl4{0.0, 0.0, 0.0, 0.0}};
-  for (int s0 = 0; s0 < G5_NS - 1 && s0 < nst; ++s0) issue(s0);
-  const int jl = 16 * wr + lr;                         // A row (column of X) of this lane
+  dbl4 acc[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) acc[c2] = dbl4{0.0, 0.0, 0.0, 0.0};
+  for (int s0 = 0; s0 < NSB - 1 && s0 < nst; ++s0) issue(s0);
+  const int jl = 16 * cw + lr;                         // A row (column of X) of this lane
   for (int st = 0; st < nst; ++st) {
-    wait_vmcnt(std::min(G5_NS - 2, nst - 1 - st) * G5_DMA);
+    wait_vmcnt(std::min(NSB - 2, nst - 1 - st) * (NDX + NDR));
     lds_barrier();
-    if (st + G5_NS - 1 < nst) issue(st + G5_NS - 1);
-    const char* b = stg + (st % G5_NS) * G5_STAGE;
+    if (st + NSB - 1 < nst) issue(st + NSB - 1);
+    const char* b = stg + (st % NSB) * STG;
 #pragma unroll
     for (int step = 0; step < G5_RB / 4; ++step) {
       const int r = 4 * step + lh;
-      const double a = *reinterpret_cast<const double*>(b + r * 512 + ((((jl >> 1) ^ ((r & 1) << 3))) << 4) + ((jl & 1) << 3));
+      const double a = *reinterpret_cast<const double*>(b + r * (16 * PPR) + ((((jl >> 1) ^ ((r & 1) << 3))) << 4) + ((jl & 1) << 3));
 #pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2)
-        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + 16384 + g5_chain_off(r, 16 * (2 * wc + c2) + lr)), acc[c2]);
+      for (int c2 = 0; c2 < NCT; ++c2)
+        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + XB + g5_chain_off(r, 16 * (NCT * cg + c2) + lr)), acc[c2]);
     }
   }
   double* out = A.partial + ((size_t)shard * A.Gs + chunk) * G5_C * A.PW;
 #pragma unroll
-  for (int c2 = 0; c2 < 2; ++c2) {
+  for (int c2 = 0; c2 < NCT; ++c2) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int j = j0 + 16 * wr + lh + 4 * i;
-      if (j < d) out[(size_t)(16 * (2 * wc + c2) + lr) * A.PW + 1 + j] = acc[c2][i];
+      const int j = j0 + 16 * cw + lh + 4 * i;
+      if (j < d) out[(size_t)(16 * (NCT * cg + c2) + lr) * A.PW + 1 + j] = acc[c2][i];
     }
   }
 }
@@ -2518,13 +2534,13 @@ hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, 
     A.qT = ws->qT;
     A.R = ws->R;
     A.Rrows = ws->Rrows;
-    const int njb = (d + G5_JB - 1) / G5_JB;
+    const int njb = (d + G5_BJB - 1) / G5_BJB;
     hipLaunchKernelGGL(k_qt_swizzle, dim3((g5_kp(d) * G5_C + 255) / 256, nsh), dim3(256), 0, st, A, d);
     auto kf = family == STK_LOGREG ? k_gemm_fwd<STK_LOGREG> : k_gemm_fwd<STK_LINREG>;
     allow_big_lds((const void*)kf);
     hipLaunchKernelGGL(kf, dim3(nblocks), dim3(64 * G5_FW), lds, st, A);
     allow_big_lds((const void*)k_gemm_bwd);
-    hipLaunchKernelGGL(k_gemm_bwd, dim3(nblocks * njb), dim3(64 * G5_NW), G5_NS * G5_STAGE, st, A, njb);
+    hipLaunchKernelGGL(k_gemm_bwd, dim3(nblocks * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
     return hipGetLastError();
   }
   if (family == STK_LOGREG) return pick_c<STK_LOGREG>(A, n, d, T, nblocks, lds, st);
