@@ -253,7 +253,12 @@ def main():
     # multi-chain estimator).  Its time counts in the ESS/s denominators.
     n_post = int(allreduce(np.array([max(ND, int(it1.max()) - A)], np.float64), "max")[0])
     t = time.perf_counter()
-    sampler.run(A + n_post)
+    while True:                      # bounded batches with a progress line (long phases under the 2.19 criterion)
+        sampler.run(A + n_post, max_steps=2000)
+        its = sampler.iterations()
+        log(f"ESS phase: {time.perf_counter() - t:.1f}s, post-warmup draws per chain min {its.min() - A} of {n_post}")
+        if its.min() >= A + n_post:
+            break
     ctx.sync()
     barrier()
     t_post = time.perf_counter() - t
