@@ -2,6 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <mutex>
+#include <set>
+#include <utility>
 #include "philox.h"
 #include "../../include/stark_hip.h"
 
@@ -123,6 +126,21 @@ __host__ __device__ inline int stack_vecs(const NutsArgs& A) { return A.uturn_ex
 __host__ __device__ inline uint32_t rng_stream(const NutsArgs& A, int gid) {
   const int s = gid / A.C;
   return (uint32_t)((A.shard_ids ? A.shard_ids[s] : s) * A.C + gid % A.C);
+}
+
+// Raise a kernel's dynamic-LDS limit to the CU's 160 KiB.  The attribute is per device, so it
+// is set once per (current device, kernel); a failure is returned to the launch that needed it.
+inline hipError_t allow_big_lds(const void* kern) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::set<std::pair<int, const void*>> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count({dev, kern})) return hipSuccess;
+  e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e == hipSuccess) done.insert({dev, kern});
+  return e;
 }
 
 }  // namespace stk

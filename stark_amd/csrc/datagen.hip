@@ -68,11 +68,7 @@ hipError_t stk_launch_gen_shard(double* X, double* yd, int32_t* yi, int64_t nrow
   int T = 64;
   while (T > 1 && (int64_t)T * d * 8 > 64 * 1024) T >>= 1;
   const size_t lds = (size_t)T * d * sizeof(double);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)k_gen_shard, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  if (const hipError_t e = allow_big_lds((const void*)k_gen_shard)) return e;
   const int64_t blocks = (nrows + T - 1) / T;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_gen_shard, dim3((unsigned)blocks), dim3(256), lds, st, X, yd, yi, nrows, d, grow0, T, seed,

@@ -826,11 +826,9 @@ template <int NCH, int CPW, int MINW = 1>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
   const size_t lds = CPW * sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp);
   if (lds > 64 * 1024) {
-    // the attribute is per device: set it on every launch that needs it (a host call, once per
-    // fused launch of up to max_steps leapfrogs) and report a failure as such
-    const hipError_t e = hipFuncSetAttribute((const void*)k_nuts_fused_schools<NCH, CPW, MINW>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
+    // the attribute is per device (allow_big_lds keys it on the current one); a failure is
+    // reported as such rather than as a generic launch failure
+    if (const hipError_t e = allow_big_lds((const void*)k_nuts_fused_schools<NCH, CPW, MINW>)) return e;
   }
   hipLaunchKernelGGL((k_nuts_fused_schools<NCH, CPW, MINW>), dim3((A.nchains + CPW - 1) / CPW), dim3(64), lds, st, A,
                      pause_at, max_steps);

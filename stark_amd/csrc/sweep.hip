@@ -2390,19 +2390,9 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
   *lds_bytes = b;
 }
 
-// Raise a kernel's dynamic-LDS limit to the CU's 160 KiB, once per kernel.
-static void allow_big_lds(const void* kern) {
-  static std::set<const void*> done;
-  if (done.insert(kern).second) hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-}
-
 template <int FAM, int C, int T, int JPT, int VEC>
 static hipError_t launch_sweep_t(const SweepArgs& A, int nblocks, size_t lds, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)k_sweep<FAM, C, T, JPT, VEC>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  if (const hipError_t e = allow_big_lds((const void*)k_sweep<FAM, C, T, JPT, VEC>)) return e;
   hipLaunchKernelGGL((k_sweep<FAM, C, T, JPT, VEC>), dim3(nblocks), dim3(256), lds, st, A);
   return hipGetLastError();
 }
@@ -2419,7 +2409,7 @@ static hipError_t pick_tile(const SweepArgs& A, int64_t n, int d, int T, int nbl
   if (var == 3) {
     if constexpr (C <= 4) {
       auto go = [&](auto kern) {
-        allow_big_lds((const void*)kern);
+        if (const hipError_t e = allow_big_lds((const void*)kern)) return e;
         hipLaunchKernelGGL(kern, dim3(nblocks), dim3(512), lds, st, A, A.LD);
         return hipGetLastError();
       };
@@ -2430,11 +2420,7 @@ static hipError_t pick_tile(const SweepArgs& A, int64_t n, int d, int T, int nbl
     return hipErrorInvalidValue;
   }
   if (var == 2) {
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute((const void*)k_sweep2<FAM, C>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
+    if (const hipError_t e = allow_big_lds((const void*)k_sweep2<FAM, C>)) return e;
     hipLaunchKernelGGL((k_sweep2<FAM, C>), dim3(nblocks), dim3(256), lds, st, A);
     return hipGetLastError();
   }
@@ -2460,7 +2446,7 @@ static const void* sweepq_kernel(int sel) {
 template <int FAM>
 static hipError_t launch_sweepm(const SweepArgs& A, int d, int nblocks, size_t lds, hipStream_t st) {
   auto go = [&](auto kern) {
-    allow_big_lds((const void*)kern);
+    if (const hipError_t e = allow_big_lds((const void*)kern)) return e;
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A, A.LD);
     return hipGetLastError();
   };
@@ -2468,21 +2454,21 @@ static hipError_t launch_sweepm(const SweepArgs& A, int d, int nblocks, size_t l
   if (sel >= 7 && (d == 100 || d == 50)) {
     const void* kern = sel == 7 ? (d == 100 ? (const void*)k_sweepx<FAM, 25, 2> : (const void*)k_sweepx<FAM, 13, 2>)
                                  : (d == 100 ? (const void*)k_sweepx<FAM, 25, 1> : (const void*)k_sweepx<FAM, 13, 1>);
-    allow_big_lds(kern);
+    if (const hipError_t e = allow_big_lds(kern)) return e;
     hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(kern)), dim3(nblocks),
                        dim3(SM_W * 64), lds, st, A);
     return hipGetLastError();
   }
   if (sel >= 3 && (d == 100 || d == 50)) {
     const void* kern = d == 100 ? sweepq_kernel<FAM, 25>(sel) : sweepq_kernel<FAM, 13>(sel);
-    allow_big_lds(kern);
+    if (const hipError_t e = allow_big_lds(kern)) return e;
     hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(kern)), dim3(nblocks),
                        dim3(SM_W * 64), lds, st, A);
     return hipGetLastError();
   }
   if (d == 100) {
     auto kern = sel == 0 ? k_sweepe<FAM, 25, 7> : (sel == 2 ? k_sweepr<FAM, 25, 7, 2> : k_sweepr<FAM, 25, 7, 1>);
-    allow_big_lds((const void*)kern);
+    if (const hipError_t e = allow_big_lds((const void*)kern)) return e;
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A);
     return hipGetLastError();
   }
@@ -2537,9 +2523,9 @@ hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, 
     const int njb = (d + G5_BJB - 1) / G5_BJB;
     hipLaunchKernelGGL(k_qt_swizzle, dim3((g5_kp(d) * G5_C + 255) / 256, nsh), dim3(256), 0, st, A, d);
     auto kf = family == STK_LOGREG ? k_gemm_fwd<STK_LOGREG> : k_gemm_fwd<STK_LINREG>;
-    allow_big_lds((const void*)kf);
+    if (const hipError_t e = allow_big_lds((const void*)kf)) return e;
     hipLaunchKernelGGL(kf, dim3(nblocks), dim3(64 * G5_FW), lds, st, A);
-    allow_big_lds((const void*)k_gemm_bwd);
+    if (const hipError_t e = allow_big_lds((const void*)k_gemm_bwd)) return e;
     hipLaunchKernelGGL(k_gemm_bwd, dim3(nblocks * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
     return hipGetLastError();
   }
