@@ -68,9 +68,16 @@ def parse():
                         "(Stan >= 2.23); stan2.19: the reference's pystan 2 NUTS, whose single test lets "
                         "trajectories resonate on this near-isotropic posterior (36 vs 11 leapfrogs per "
                         "transition, DESIGN.md section 4)")
-    p.add_argument("--second-criterion", choices=["stan2.23", "stan2.19", "none"], default="none",
+    p.add_argument("--second-criterion", choices=["stan2.23", "stan2.19", "none"], default="stan2.19",
                    help="after the main run: a second adaptation + ESS phase on the same data with this "
-                        "NUTS criterion, reported as ess_second_criterion")
+                        "NUTS criterion (default: the reference's pystan 2 sampler, Stan 2.19.1), reported as "
+                        "ess_second_criterion")
+    p.add_argument("--second-jitter", type=float, default=0.0,
+                   help="stepsize_jitter of the second run (0: pystan 2's default, the reference's setting)")
+    p.add_argument("--second-draws", type=int, default=100, help="post-warmup draws per chain of the second run")
+    p.add_argument("--second-budget-s", type=float, default=300.0,
+                   help="wall-time bound of the second run (warmup + draws); past it the run stops and the line "
+                        "says so instead of an ESS")
     p.add_argument("--seed", type=int, default=20240)
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -87,8 +94,16 @@ def cpu_baseline(d, rows_per_shard, shards, seconds, family="logistic"):
     cores = len(os.sched_getaffinity(0))
     workers = max(1, min(shards, cores))
     ctx = mp.get_context("spawn")
-    with ctx.Pool(workers) as pool:
+    pool = ctx.Pool(workers)
+    try:
         rates = pool.starmap(_cpu_worker, [(d, seconds, w, family) for w in range(workers)])
+        # close + join: the workers exit on their own (Pool.__exit__ would terminate() them, i.e.
+        # SIGTERM processes that may run under a profiler's signal handler)
+        pool.close()
+        pool.join()
+    except BaseException:
+        pool.terminate()
+        raise
     sample_rows = rates[0][1]
     per_worker_grads = [r[0] * sample_rows / rows_per_shard for r in rates]   # full-shard grads/s
     return {"value": float(sum(per_worker_grads)), "unit": "gradient evals/sec (whole node)",
@@ -196,7 +211,7 @@ def main():
             return arr
         dev = sdist._device_for_backend()
         t_ = torch.from_numpy(np.ascontiguousarray(arr, np.float64)).to(dev)
-        dist.all_reduce(t_, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        dist.all_reduce(t_, op={"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}.get(op, dist.ReduceOp.SUM))
         arr[...] = t_.cpu().numpy()
         return arr
 
@@ -264,17 +279,23 @@ def main():
     t_post = time.perf_counter() - t
     info = sampler.info()
     C = a.chains
+    # the draws stay in HBM: library buffer -> device tensor -> RCCL all-gather -> device combine
+    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else None
+    cols = np.concatenate([np.arange(c * n_samp, c * n_samp + n_post) for c in range(C)])
+    cols_t = torch.as_tensor(cols, device=dev)
     local = {}
     stats = []
     for s in range(spr):
-        dr, st = sampler.draws(s)
-        cols = np.concatenate([np.arange(c * n_samp, c * n_samp + n_post) for c in range(C)])
-        local[shard_ids[s]] = np.ascontiguousarray(dr[:, cols])
-        stats.append(st[cols])
+        full = sampler.draws_device(s)
+        local[shard_ids[s]] = full.index_select(1, cols_t).contiguous()
+        stats.append(sampler.draws(s)[1][cols])
     stats = np.vstack(stats)
     t = time.perf_counter()
-    allp = sdist.all_gather_partitions(local, a.shards)       # one all-gather (RCCL on GPUs)
+    allp_dev = sdist.all_gather_partitions(local, a.shards, as_tensor=True)   # one all-gather (RCCL on GPUs)
+    if allp_dev.is_cuda:
+        torch.cuda.synchronize(allp_dev.device)
     t_gather = time.perf_counter() - t
+    allp = list(allp_dev.cpu().numpy())          # host copies: Laplace start point, CPU combine, ESS
     eps, _ = sampler.adaptation()
     # full-data posterior reference (logistic, flat priors): MAP + inverse Hessian from the
     # GPU gradient summed over every shard of every rank (tools/laplace.py)
@@ -288,30 +309,45 @@ def main():
         log(f"full-data Laplace reference in {time.perf_counter() - t:.1f}s")
     second = None
     if a.second_criterion != "none" and a.second_criterion != a.nuts_criterion:
-        # the same data, warmup length and post-warmup draws, another U-turn criterion
+        # the same data, warmup length and shard RNG keys under another NUTS criterion / jitter
+        # (default: the reference's pystan 2 sampler, Stan 2.19.1 with stepsize_jitter 0), in
+        # bounded step batches under a wall-time budget
+        ND2 = a.second_draws
         t = time.perf_counter()
-        s2 = model.sampler(num_warmup=A, num_samples=ND, chains=a.chains, seed=a.seed + 1, shard_ids=shard_ids,
-                           stepsize_jitter=a.stepsize_jitter, nuts_criterion=a.second_criterion)
-        s2.run(A)
-        ctx.sync()
-        barrier()
-        t2_adapt = time.perf_counter() - t
-        t = time.perf_counter()
-        s2.run(A + ND)
-        ctx.sync()
-        barrier()
-        t2_post = time.perf_counter() - t
-        loc2, st2 = {}, []
-        for s_ in range(spr):
-            dr, st = s2.draws(s_)
-            loc2[shard_ids[s_]] = np.ascontiguousarray(dr)
-            st2.append(st)
-        allp2 = sdist.all_gather_partitions(loc2, a.shards)
-        st2 = np.vstack(st2)
-        second = {"allp": allp2, "t_adapt": t2_adapt, "t_post": t2_post,
-                  "lf": float(st2[:, 3].mean()), "div": s2.info()["divergent"]}
+        s2 = model.sampler(num_warmup=A, num_samples=ND2, chains=a.chains, seed=a.seed + 1, shard_ids=shard_ids,
+                           stepsize_jitter=a.second_jitter, nuts_criterion=a.second_criterion)
+        phase, completed = {}, True
+        for target in (A, A + ND2):
+            t_ph = time.perf_counter()
+            while True:
+                s2.run(target, max_steps=2000)
+                its = s2.iterations()
+                done = float(allreduce(np.array([float(its.min() >= target)]), "min")[0]) > 0
+                over = float(allreduce(np.array([float(time.perf_counter() - t > a.second_budget_s)]), "max")[0]) > 0
+                log(f"second criterion {a.second_criterion}: {time.perf_counter() - t:.1f}s, transitions per chain "
+                    f"min {its.min()} of {target}")
+                if done or over:
+                    break
+            ctx.sync()
+            barrier()
+            phase[target] = time.perf_counter() - t_ph
+            if not done:
+                completed = False
+                break
+        if not completed:
+            second = {"status": f"stopped at the {a.second_budget_s:.0f} s budget", "iterations_min": int(its.min()),
+                      "seconds": time.perf_counter() - t}
+        else:
+            loc2, st2 = {}, []
+            for s_ in range(spr):
+                loc2[shard_ids[s_]] = s2.draws_device(s_)
+                st2.append(s2.draws(s_)[1])
+            allp2 = sdist.all_gather_partitions(loc2, a.shards, as_tensor=True)
+            st2 = np.vstack(st2)
+            second = {"allp": allp2, "t_adapt": phase[A], "t_post": phase[A + ND2], "nd": ND2,
+                      "lf": float(st2[:, 3].mean()), "div": s2.info()["divergent"]}
         s2.close()
-        log(f"second criterion {a.second_criterion}: adaptation {t2_adapt:.1f}s, {ND} draws {t2_post:.1f}s")
+        log(f"second criterion {a.second_criterion}: {time.perf_counter() - t:.1f}s")
     lin = None
     if a.family == "linear" and not a.no_accuracy:
         # flat-prior linear regression: the full-data posterior of (alpha, beta) in closed form
@@ -345,16 +381,22 @@ def main():
     from stark_amd import diagnostics
     P = allp[0].shape[0]
     comb_ms = []
-    for _ in range(4):                                        # the first call also sizes the scratch buffers
+    for _ in range(6):      # device draws in, device result out; the first call also sizes the scratch buffers
         t = time.perf_counter()
-        comb, used = engine.consensus(allp, ctx, separate_lp=True)
+        comb_t, used = engine.consensus(allp_dev, ctx, separate_lp=True)
         comb_ms.append(1e3 * (time.perf_counter() - t))
+    comb = comb_t.cpu().numpy() if hasattr(comb_t, "cpu") else comb_t
+    t = time.perf_counter()
+    comb_host, _ = engine.consensus(allp, ctx, separate_lp=True)     # the host-buffer API, for comparison
+    comb_host_ms = 1e3 * (time.perf_counter() - t)
+    assert np.array_equal(comb_host, comb)
     comb_joint, _ = engine.consensus(allp, ctx)               # the reference's joint weights (lp__ in)
 
-    def min_ess(x):
-        return float(np.nanmin([diagnostics.ess(x[p].reshape(C, n_post)) for p in range(x.shape[0])]))
+    def min_ess(x, floor=False, n=n_post):
+        return float(np.nanmin([diagnostics.ess(x[p].reshape(C, n), floor=floor) for p in range(x.shape[0])]))
 
     ess_c = min_ess(comb[:-1])                                 # lp__ excluded
+    ess_c_floor = min_ess(comb[:-1], floor=True)
     ess_s0 = min_ess(allp[0][:-1])
     t_sampling = t_wsteps + elapsed + t_post
     truth = np.concatenate([[0.0], engine.Model.gen_beta(a.seed, a.d)])
@@ -387,11 +429,18 @@ def main():
             "sd_ratio_median": float(np.median(comb[:k].std(1) / fsd)),
             "truth": zz(truth[:k] - fm, fsd),
             "note": "alpha, beta vs the closed-form flat-prior posterior (multivariate t) of all N rows"}
-    if second is not None:
-        comb2, _ = engine.consensus(second["allp"], ctx, separate_lp=True)
-        ess2 = float(np.nanmin([diagnostics.ess(comb2[p].reshape(C, ND)) for p in range(comb2.shape[0] - 1)]))
-        second_line = {"nuts_criterion": a.second_criterion, "ess_per_sec": ess2 / (second["t_adapt"] + second["t_post"]),
-                       "min_ess": ess2, "ess_per_sec_post_warmup": ess2 / second["t_post"],
+    if second is not None and "allp" not in second:
+        second_line = {"nuts_criterion": a.second_criterion, "stepsize_jitter": a.second_jitter, **second}
+    elif second is not None:
+        comb2_t, _ = engine.consensus(second["allp"], ctx, separate_lp=True)
+        comb2 = comb2_t.cpu().numpy() if hasattr(comb2_t, "cpu") else comb2_t
+        ess2 = min_ess(comb2[:-1], n=second["nd"])
+        second_line = {"nuts_criterion": a.second_criterion, "stepsize_jitter": a.second_jitter,
+                       "note": "the reference's sampler settings (pystan 2 = Stan 2.19.1 NUTS, no step-size jitter) on "
+                               "the same data, warmup length and shard RNG keys",
+                       "ess_per_sec": ess2 / (second["t_adapt"] + second["t_post"]),
+                       "min_ess": ess2, "min_ess_floored": min_ess(comb2[:-1], floor=True, n=second["nd"]),
+                       "ess_per_sec_post_warmup": ess2 / second["t_post"], "post_warmup_draws_per_chain": second["nd"],
                        "leapfrogs_per_transition": second["lf"], "divergent": second["div"],
                        "seconds": {"adaptation": second["t_adapt"], "post_warmup_draws": second["t_post"]}}
         if lap is not None:
@@ -433,14 +482,20 @@ def main():
             traffic = None
     hbm = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": (gbs / HBM_PEAK_GBS) if gbs else None}
     if mfma:
-        roof = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": (tfs / FP64_PEAK_TFS) if tfs else None, "traffic": traffic,
+        # arithmetic intensity 4 C d / (8 d + 4) = 7.96 flop/B at C = 16, d = 100: below the fp64
+        # machine balance (78.6 TF / 8 TB/s = 9.8 flop/B), so the roofline that bounds the sweep is
+        # HBM; the fp64-MFMA figure is reported beside it
+        intensity = flops_per_launch / bytes_per_launch
+        balance = FP64_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
+        mf = {"achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": (tfs / FP64_PEAK_TFS) if tfs else None,
+              "peak_measured": FP64_MFMA_MEASURED_TFS,
+              "peak_measured_instruction": "v_mfma_f64_16x16x4_f64 (the kernel's)",
+              "frac_of_measured": (tfs / FP64_MFMA_MEASURED_TFS) if tfs else None}
+        prim, sec, sec_name = (hbm, mf, "mfma") if intensity < balance else (mf, hbm, "hbm")
+        roof = {"bound": "hbm" if intensity < balance else "mfma", **prim, "traffic": traffic,
                 "kernel": f"{kname}<{fam}> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
                 "algorithmic_flops_per_launch": flops_per_launch, "algorithmic_bytes_per_launch": bytes_per_launch,
-                "peak_measured": FP64_MFMA_MEASURED_TFS,
-                "peak_measured_instruction": "v_mfma_f64_16x16x4_f64 (the kernel's)",
-                "frac_of_measured": (tfs / FP64_MFMA_MEASURED_TFS) if tfs else None,
-                "peak_measured_4x4x4_4b": FP64_MFMA4_MEASURED_TFS, "hbm": hbm}
+                "intensity_flop_per_byte": intensity, "machine_balance_flop_per_byte": balance, sec_name: sec}
     else:
         roof = dict(bound="hbm", **{k: v for k, v in hbm.items()}, traffic=traffic,
                     kernel=f"k_sweep3<{fam},{a.chains}>", avg_launch_ms=avg_ms,
@@ -450,7 +505,7 @@ def main():
     # CPU twin (transition-identical, tests/test_gpu_nuts.py) spends the same gradients per ESS
     total_grads = info["grad_evals"] * world
     cpu = None
-    if not a.no_cpu_baseline and world == 1:
+    if not a.no_cpu_baseline:          # rank 0 only (the other ranks returned above), at every world size
         try:
             cpu = cpu_baseline(a.d, rows_per_shard, a.shards, a.cpu_baseline_seconds, a.family)
             cpu["ess_per_sec"] = cpu["value"] * ess_c / total_grads
@@ -479,6 +534,9 @@ def main():
                    "parallelism": f"shard-dp{world}"},
         "ess_per_sec": ess_c / (t_adapt + t_sampling),
         "min_ess": ess_c,
+        "ess_per_sec_floored": ess_c_floor / (t_adapt + t_sampling),
+        "ess_floor_note": ("*_floored: the same ESS with the tau_hat >= 1/log10(draws) bound of Stan releases after 2.19 "
+                           "(ess_per_sec is Stan 2.19's estimator, which has no such bound)"),
         "ess_method": ("min over alpha, beta (lp__ excluded) of Stan 2.19's multi-chain ESS of the consensus draws "
                        f"({C} combined chains x {n_post} post-warmup draws; combined chain c = chain c of every "
                        "shard), divided by the whole sampling wall time: warmup/adaptation + the timed steps + the "
@@ -495,10 +553,12 @@ def main():
         "rows_x_chains_per_sec": grads * rows_per_shard / elapsed,
         "roofline": roof,
         "cpu_baseline": cpu,
-        "combine": {"gpu_ms": min(comb_ms[1:]), "gpu_ms_first_call": comb_ms[0], "shards": a.shards, "P": P,
+        "combine": {"gpu_ms": float(np.median(comb_ms[1:])), "gpu_ms_min": min(comb_ms[1:]),
+                    "gpu_ms_first_call": comb_ms[0], "host_buffers_ms": comb_host_ms, "shards": a.shards, "P": P,
                     "draws": C * n_post, "all_gather_ms": 1e3 * t_gather,
-                    "note": "engine.consensus(separate_lp=True) on host buffers: host->device copy of the draws, "
-                            "the combine kernels, the result copied back"},
+                    "note": "engine.consensus(separate_lp=True) on the all-gathered DEVICE draws (no host copy), the "
+                            "result left in HBM; wall time of the call (median of 5 after the first); host_buffers_ms: "
+                            "the same combine through host numpy buffers (H2D + D2H copies included)"},
         "setup_s": {"datagen": t_gen, "adaptation": t_adapt, "post_warmup_draws": t_post},
         "timed_window_monotonic_ns": [w0, w1],     # tools/rocpd_summary.py window: the kernel trace's dispatches in it
         "divergent": info["divergent"],

@@ -103,6 +103,9 @@ typedef struct {
                                 junction of the merged halves that Stan >= 2.23 adds (base_nuts
                                 build_tree / transition), which stop the trajectories that the single
                                 test lets run on near-isotropic Gaussian posteriors */
+  int32_t chains_per_wave;   /* 8-schools fused kernel: chains packed per 64-lane wave, 0 (default) =
+                                the most that fit (4 for D <= 16, 2 for D <= 32, else 1); 1 or 2 cap
+                                it (test hook: the packing changes no bit of the draws) */
 } stk_config;
 
 typedef struct {
@@ -197,7 +200,16 @@ STK_API int stk_transition(stk_model* m, int shard, double* q, int32_t C, uint64
                            double eps, const double* inv_metric, int32_t max_depth, double* lp, double* stats);
 
 /* ---- consensus combine: stark/stark.py:7-21, 66-70 ---- */
-/* draws: nshards x P x S.  shard_used[s] = 0 for shards left out because of NaN draws. */
+/* draws: nshards x P x S (host or device memory).  shard_used[s] = 0 for shards left out
+ * because of NaN draws.  Singular matrices (STK_E_LINALG, numpy's LinAlgError):
+ *   - stk_consensus / _blocked / _products invert each sample covariance and sum W, which are
+ *     symmetric positive (semi)definite by construction, by diagonal-pivot block Gauss-Jordan and
+ *     report a pivot <= 0 or NaN as singular.  A rank-deficient covariance (S - 1 < P, collinear
+ *     rows) therefore raises here, where np.linalg.inv's LU usually returns a huge finite
+ *     "inverse" built from rounding noise;
+ *   - stk_consensus_solve takes the caller's sum W as ANY square matrix (symmetric or not) and
+ *     inverts it as np.linalg.inv does, by partial pivoting, singular only on an exactly zero
+ *     pivot. */
 STK_API int stk_consensus_products(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S,
                                    double* sum_w, double* sum_wtheta, int32_t* shard_used);
 STK_API int stk_consensus_solve(stk_ctx* ctx, const double* sum_w, const double* sum_wtheta, int32_t P,

@@ -47,7 +47,8 @@ class Config(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("init", ctypes.c_void_p), ("inv_metric", ctypes.c_void_p),
                 ("skip_init_stepsize", ctypes.c_int32), ("iter_offset", ctypes.c_int32),
                 ("save_warmup", ctypes.c_int32), ("shard_ids", ctypes.c_void_p),
-                ("stepsize_jitter", ctypes.c_double), ("nuts_criterion", ctypes.c_int32)]
+                ("stepsize_jitter", ctypes.c_double), ("nuts_criterion", ctypes.c_int32),
+                ("chains_per_wave", ctypes.c_int32)]
 
 
 class RunInfo(ctypes.Structure):

@@ -37,8 +37,9 @@ hipError_t stk_launch_gen_shard(double* X, double* yd, int32_t* yi, int64_t nrow
 hipError_t stk_launch_consensus_products(const double* X, int nshards, int P, int S, const int32_t* blk, double* mean,
                                          int32_t* rowbad, int32_t* used, int32_t* status, double* cov, double* W,
                                          double* work, double* sum_w, double* sum_wtheta, hipStream_t st);
+size_t stk_general_inverse_work_bytes(int P);
 hipError_t stk_launch_consensus_solve(const double* sum_w, const double* sum_wtheta, int P, int S, double* inv_buf,
-                                      double* work, int32_t* status, double* out, hipStream_t st);
+                                      double* work, int32_t* status, double* out, hipStream_t st, bool general);
 size_t stk_spd_inverse_work_bytes(int P, int batch);
 
 // ---------------------------------------------------------------- errors
@@ -520,6 +521,8 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   ARG_CHECK(cfg->stepsize > 0, "stepsize must be positive");
   ARG_CHECK(cfg->stepsize_jitter >= 0 && cfg->stepsize_jitter <= 1, "stepsize_jitter must be in [0, 1]");
   ARG_CHECK(cfg->nuts_criterion == 0 || cfg->nuts_criterion == 1, "nuts_criterion must be 0 (Stan 2.19) or 1 (Stan >= 2.23)");
+  ARG_CHECK(cfg->chains_per_wave >= 0 && cfg->chains_per_wave <= 4 && cfg->chains_per_wave != 3,
+            "chains_per_wave must be 0, 1, 2 or 4");
   stk_ctx* ctx = m->ctx;
   STK_HIP_CHECK(hipSetDevice(ctx->device));
   const int nch = stk_nch_for(m->Dmax);
@@ -562,6 +565,7 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   A.seed = cfg->seed;
   A.jitter = cfg->stepsize_jitter;
   A.uturn_ext = cfg->nuts_criterion;
+  A.cpw_cap = cfg->chains_per_wave;
   A.S_total = cfg->chains * cfg->num_samples;
   A.Pmax = m->Pmax;
   A.shards = m->sh_dev.as<ShardDev>();
@@ -985,10 +989,10 @@ struct CombineBufs {
   double *X, *mean, *cov, *W, *work, *sw, *swt, *inv, *out;
   int32_t *rowbad, *used, *status, *blk;
 };
-int combine_bufs(stk_ctx* ctx, int nshards, int P, int S, CombineBufs* b) {
+int combine_bufs(stk_ctx* ctx, int nshards, int P, int S, CombineBufs* b, bool general = false) {
   DevBuf* B = ctx->scratch;
   const size_t per = (size_t)P * S, pp = (size_t)P * P;
-  const size_t wk = stk_spd_inverse_work_bytes(P, nshards);
+  const size_t wk = std::max(stk_spd_inverse_work_bytes(P, nshards), general ? stk_general_inverse_work_bytes(P) : 0);
   RC(B[8].ensure(sizeof(double) * (per * nshards + per * 2 + (size_t)P * nshards)));
   RC(B[9].ensure(sizeof(double) * (pp * nshards * 2 + pp * 2) + wk + 16));
   RC(B[10].ensure(sizeof(int32_t) * ((size_t)P * nshards + 2 * (size_t)nshards + 2 + (size_t)P) + 64));
@@ -1038,7 +1042,7 @@ int consensus_run(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P,
   STK_HIP_CHECK(stk_launch_consensus_products(b.X, nshards, P, S, row_block ? b.blk : nullptr, b.mean, b.rowbad,
                                               b.used, b.status, b.cov, b.W, b.work, b.sw, b.swt, st));
   if (out)
-    STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status + nshards, b.out, st));
+    STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status + nshards, b.out, st, false));
   std::vector<int32_t> h(2 * nshards + 1, 0);
   STK_HIP_CHECK(hipMemcpyAsync(h.data(), b.used, sizeof(int32_t) * (2 * nshards + (out ? 1 : 0)), hipMemcpyDeviceToHost, st));
   STK_HIP_CHECK(hipStreamSynchronize(st));
@@ -1067,10 +1071,11 @@ int stk_consensus_solve(stk_ctx* ctx, const double* sum_w, const double* sum_wth
   hipStream_t st = ctx->stream;
   const size_t per = (size_t)P * S;
   CombineBufs b;
-  RC(combine_bufs(ctx, 1, P, S, &b));
+  RC(combine_bufs(ctx, 1, P, S, &b, true));
   STK_HIP_CHECK(hipMemcpyAsync(b.sw, sum_w, sizeof(double) * P * P, hipMemcpyDefault, st));
   STK_HIP_CHECK(hipMemcpyAsync(b.swt, sum_wtheta, sizeof(double) * per, hipMemcpyDefault, st));
-  STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status, b.out, st));
+  // the caller's sum W: any invertible matrix, inverted by partial pivoting as np.linalg.inv
+  STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status, b.out, st, true));
   int32_t hs = 0;
   STK_HIP_CHECK(hipMemcpyAsync(&hs, b.status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
   STK_HIP_CHECK(hipMemcpyAsync(out, b.out, sizeof(double) * per, hipMemcpyDefault, st));

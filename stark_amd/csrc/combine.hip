@@ -21,7 +21,8 @@
 //   k_sum_w          sum_s W_s in shard order (NaN shards hold W = 0)
 //   k_mgemm<WTheta>  sum_s W_s theta_s as ONE GEMM with K = shards x P:
 //                    [W_1 .. W_S] (P x SP) . [theta_1; ..; theta_S] (SP x S), NaN shards skipped
-//   k_spd_inverse + k_mgemm<Plain>  out = inv(sum W) . sum W theta
+//   k_spd_inverse + k_mgemm<Plain>  out = inv(sum W) . sum W theta (the public stk_consensus_solve,
+//                    whose sum W comes from the caller, inverts it by partial pivoting instead)
 // k_mgemm: fp64 MFMA, one 16 x 16 NB output tile per block, K split over the block's waves,
 // every output a fixed-order sum (cov_s only on the upper tiles, stored both ways).
 #include "common.h"
@@ -573,8 +574,18 @@ hipError_t stk_launch_consensus_products(const double* X, int nshards, int P, in
 
 // out [P][S] = inv(sum_w) . sum_wtheta (inv_buf [P][P], work for P > 128)
 hipError_t stk_launch_consensus_solve(const double* sum_w, const double* sum_wtheta, int P, int S, double* inv_buf,
-                                      double* work, int32_t* status, double* out, hipStream_t st) {
-  hipError_t e = stk_launch_spd_inverse(sum_w, inv_buf, work, P, 1, nullptr, status, st);
+                                      double* work, int32_t* status, double* out, hipStream_t st, bool general) {
+  // general: a caller's sum W (stk_consensus_solve) need not be symmetric positive definite, so it
+  // is inverted as np.linalg.inv does, by partial-pivot elimination (k_gj_inverse: singular only on
+  // an exactly zero pivot, as LAPACK getrf); inside stk_consensus sum W is a sum of SPD inverses
+  hipError_t e;
+  if (general) {
+    hipLaunchKernelGGL(k_gj_inverse, dim3(1), dim3(1024), 0, st, sum_w, work, inv_buf, P, nullptr, status);
+    e = hipGetLastError();
+  } else {
+    e = stk_launch_spd_inverse(sum_w, inv_buf, work, P, 1, nullptr, status, st);
+  }
   if (e != hipSuccess) return e;
   return mgemm<PlainLd, 2, 2, false>(PlainLd{inv_buf, sum_wtheta, out, P, S, S}, P, S, P, 1, st);
 }
+size_t stk_general_inverse_work_bytes(int P) { return sizeof(double) * (size_t)P * 2 * P; }

@@ -115,6 +115,7 @@ struct NutsArgs {
   const int* shard_ids;  // nullptr or global shard index per local shard (RNG stream keys)
   double jitter;         // stepsize_jitter (0: off)
   int uturn_ext;         // nuts_criterion: 1 = Stan >= 2.23 extra U-turn checks
+  int cpw_cap;           // chains_per_wave cap of the fused 8-schools kernel (0: none)
 };
 
 // Stack vectors per level in use: the Stan >= 2.23 junction checks need SV_PB / SV_PE / SV_PSE,

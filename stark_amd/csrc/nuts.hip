@@ -835,15 +835,11 @@ static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps,
   return hipGetLastError();
 }
 
-// chains per wave of the fused 8-schools kernel: 4 for D <= 16, 2 for D <= 32 (STARK_FUSED_CPW
-// overrides, for measurements)
-static int fused_cpw(int Dp) {
-  static const int forced = [] {
-    const char* e = getenv("STARK_FUSED_CPW");
-    return e ? atoi(e) : 0;
-  }();
-  int c = Dp <= 16 ? 4 : (Dp <= 32 ? 2 : 1);
-  if (forced == 1 || forced == 2 || forced == 4) c = std::min(c, forced);
+// chains per wave of the fused 8-schools kernel: 4 for D <= 16, 2 for D <= 32, capped by the
+// sampler's chains_per_wave (stk_config; 0 = no cap)
+static int fused_cpw(const NutsArgs& A) {
+  int c = A.Dp <= 16 ? 4 : (A.Dp <= 32 ? 2 : 1);
+  if (A.cpw_cap > 0) c = std::min(c, A.cpw_cap);
   return c;
 }
 
@@ -872,17 +868,10 @@ hipError_t stk_launch_nuts_step(const NutsArgs& A, int nch, int step_id, int pau
 }
 
 hipError_t stk_launch_nuts_fused(const NutsArgs& A, int nch, int pause_at, int max_steps, hipStream_t st) {
-  static const int minw = [] {
-    const char* e = getenv("STARK_FUSED_MINW");     // measurements: 2 = two waves per SIMD (spills)
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
   if (nch == 1) {
-    switch (fused_cpw(A.Dp) * 10 + minw) {
-      case 41: return launch_fused_t<1, 4>(A, pause_at, max_steps, st);
-      case 42: return launch_fused_t<1, 4, 2>(A, pause_at, max_steps, st);
-      case 21: return launch_fused_t<1, 2>(A, pause_at, max_steps, st);
-      case 22: return launch_fused_t<1, 2, 2>(A, pause_at, max_steps, st);
-      case 12: return launch_fused_t<1, 1, 2>(A, pause_at, max_steps, st);
+    switch (fused_cpw(A)) {
+      case 4: return launch_fused_t<1, 4>(A, pause_at, max_steps, st);
+      case 2: return launch_fused_t<1, 2>(A, pause_at, max_steps, st);
       default: return launch_fused_t<1, 1>(A, pause_at, max_steps, st);
     }
   }

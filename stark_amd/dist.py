@@ -40,21 +40,33 @@ def _device_for_backend():
     return torch.device("cpu")
 
 
-def all_gather_partitions(local: dict, n_partitions: int):
-    """local: {partition index: 2-D float64 array} -- whatever partitions this rank holds
-    (round-robin p % world for the driver, contiguous blocks for bench.py).  Returns the
-    list over all partitions: one all_gather of a padded [slots, rows, cols] fp64 tensor per
-    rank, after a tiny object collective that tells every rank who holds which partition."""
+def all_gather_partitions(local: dict, n_partitions: int, as_tensor: bool = False):
+    """local: {partition index: 2-D float64 array or device tensor} -- whatever partitions
+    this rank holds (round-robin p % world for the driver, contiguous blocks for bench.py).
+    Returns the list over all partitions: one all_gather of a padded [slots, rows, cols] fp64
+    tensor per rank, after a tiny object collective that tells every rank who holds which
+    partition.
+
+    as_tensor: return ONE [n_partitions, rows, cols] fp64 tensor on this rank's device instead
+    (all partitions must share one shape, as the combine requires, stark/stark.py:20): the
+    gathered draws stay in HBM and go straight into the device combine (engine.consensus)."""
     rank, ws = world()
     import torch.distributed as _d
     if not (_d.is_available() and _d.is_initialized()):
+        if as_tensor:
+            import torch
+            parts = [torch.as_tensor(local[p], dtype=torch.float64) for p in range(n_partitions)]
+            dev = next((t.device for t in parts if t.is_cuda), None)
+            if dev is None and torch.cuda.is_available():
+                dev = torch.device("cuda", torch.cuda.current_device())
+            return torch.stack([t.to(dev) for t in parts]).contiguous()
         return [local[p] for p in range(n_partitions)]
     # an initialised group runs the collective even at world size 1 (same code path as N > 1)
     import torch
     import torch.distributed as dist
     dev = _device_for_backend()      # before the object collective: it sends on the current device
     held = [None] * ws
-    dist.all_gather_object(held, {int(p): tuple(a.shape) for p, a in local.items()})
+    dist.all_gather_object(held, {int(p): tuple(int(v) for v in a.shape) for p, a in local.items()})
     where, shapes = {}, {}
     for r, dct in enumerate(held):
         for k, p in enumerate(sorted(dct)):
@@ -68,10 +80,15 @@ def all_gather_partitions(local: dict, n_partitions: int):
     slots = max(1, max(len(dct) for dct in held))
     buf = torch.zeros((slots, rmax, cmax), dtype=torch.float64, device=dev)
     for k, p in enumerate(sorted(local)):
-        a = torch.as_tensor(np.ascontiguousarray(local[p]), dtype=torch.float64)
-        buf[k, : a.shape[0], : a.shape[1]] = a.to(dev)
+        a = local[p] if isinstance(local[p], torch.Tensor) else torch.as_tensor(np.ascontiguousarray(local[p]))
+        buf[k, : a.shape[0], : a.shape[1]] = a.to(dev, torch.float64)
     out = [torch.empty_like(buf) for _ in range(ws)]
     dist.all_gather(out, buf)
+    if as_tensor:
+        if len(set(shapes.values())) != 1:
+            raise ValueError(f"as_tensor: partitions must share one shape, got {sorted(set(shapes.values()))}")
+        rr, cc = shapes[0]
+        return torch.stack([out[where[p][0]][where[p][1], :rr, :cc] for p in range(n_partitions)]).contiguous()
     res = []
     for p in range(n_partitions):
         r, k = where[p]

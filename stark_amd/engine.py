@@ -122,7 +122,7 @@ def make_config(num_warmup=1000, num_samples=1000, chains=1, max_depth=10, adapt
                 adapt_kappa=0.75, adapt_t0=10.0, stepsize=1.0, init_radius=2.0, adapt_init_buffer=75,
                 adapt_term_buffer=50, adapt_window=25, adapt_engaged=True, seed=1234, init=None,
                 inv_metric=None, skip_init_stepsize=False, iter_offset=0, shard_ids=None,
-                save_warmup=False, stepsize_jitter=0.0, nuts_criterion="stan2.19"):
+                save_warmup=False, stepsize_jitter=0.0, nuts_criterion="stan2.19", chains_per_wave=0):
     """Stan sampler settings (pystan 2 `sampling()` keywords + control block).
     nuts_criterion: "stan2.19" (the reference's pystan 2: one U-turn test per merged subtree)
     or "stan2.23" (plus the checks across subtree junctions of Stan >= 2.23)."""
@@ -135,6 +135,7 @@ def make_config(num_warmup=1000, num_samples=1000, chains=1, max_depth=10, adapt
     if nuts_criterion not in crit:
         raise ValueError(f"nuts_criterion must be 'stan2.19' or 'stan2.23', got {nuts_criterion!r}")
     c.nuts_criterion = crit[nuts_criterion]
+    c.chains_per_wave = int(chains_per_wave)
     c.adapt_init_buffer, c.adapt_term_buffer, c.adapt_window = adapt_init_buffer, adapt_term_buffer, adapt_window
     c.adapt_engaged = int(bool(adapt_engaged))
     c.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
@@ -356,6 +357,19 @@ class Sampler:
         check(_lib.load().stk_sampler_draws(self._h, shard, out.ctypes.data, st.ctypes.data))
         return out, st
 
+    def draws_device(self, shard: int, out=None):
+        """The draws of one shard, P x (chains * num_samples), copied device-to-device into a
+        torch fp64 tensor on the context's GPU (allocated if `out` is None); no host copy."""
+        import torch
+        S = self.cfg.chains * self.cfg.num_samples
+        if out is None:
+            out = torch.empty((self.model.P[shard], S), dtype=torch.float64, device=f"cuda:{self.model.ctx.device}")
+        if tuple(out.shape) != (self.model.P[shard], S) or out.dtype != torch.float64 or not out.is_cuda:
+            raise ValueError(f"out must be a cuda fp64 tensor of shape {(self.model.P[shard], S)}")
+        torch.cuda.current_stream(out.device).synchronize()
+        check(_lib.load().stk_sampler_draws(self._h, shard, _ptr(out), None))
+        return out
+
     def unconstrained(self, shard: int):
         n = self.cfg.num_samples + (self.cfg.num_warmup if self.cfg.save_warmup else 0)
         out = np.empty((self.cfg.chains, n, self.model.D[shard]))
@@ -409,9 +423,35 @@ def _stack(draws):
     return np.ascontiguousarray(np.stack(d)), d[0].shape
 
 
+def _device_stack(draws):
+    """draws as ONE contiguous [nshards, P, S] fp64 cuda tensor, or None for host input."""
+    try:
+        import torch
+    except ImportError:          # pragma: no cover
+        return None
+    if isinstance(draws, torch.Tensor):
+        t = draws
+    elif isinstance(draws, (list, tuple)) and draws and all(isinstance(x, torch.Tensor) for x in draws):
+        if len({tuple(x.shape) for x in draws}) != 1:
+            raise ValueError(f"shards must share one (P, S) shape, got {sorted({tuple(x.shape) for x in draws})}")
+        t = torch.stack(list(draws))
+    else:
+        return None
+    if t.dim() != 3:
+        raise ValueError("draws tensor must be [nshards, P, S]")
+    if not t.is_cuda:
+        return None
+    return t.to(torch.float64).contiguous()
+
+
 def consensus(draws, ctx: Context | None = None, separate_lp: bool = False):
     """(sum_s W_s)^-1 sum_s W_s theta_s, W_s = inv(cov(theta_s)): stark/stark.py:66-70 over
     the reducer stark/stark.py:7-21.  Returns (P x S, shard_used).
+
+    draws: a list of P x S host arrays, or device-resident draws -- a [nshards, P, S] cuda
+    tensor (e.g. dist.all_gather_partitions(..., as_tensor=True)) or a list of P x S cuda
+    tensors.  Device draws are combined where they lie (no host round trip) and the result is
+    a P x S cuda tensor on the same device.
 
     separate_lp: the last row (lp__, which fit.extract() hands the reference's combine,
     stark/stark.py:49-56) gets a 1 x 1 weight block of its own instead of joining the parameter
@@ -420,6 +460,23 @@ def consensus(draws, ctx: Context | None = None, separate_lp: bool = False):
     the joint combine by a multiple of that offset.  Block weights are exact for a Gaussian
     posterior, where lp__ is uncorrelated with the parameters."""
     ctx = ctx or default_context()
+    dev = _device_stack(draws)
+    if dev is not None:
+        import torch
+        ns, P, S = (int(v) for v in dev.shape)
+        out_t = torch.empty((P, S), dtype=torch.float64, device=dev.device)
+        used = np.empty(ns, np.int32)
+        torch.cuda.current_stream(dev.device).synchronize()    # the library runs on its own stream
+        if separate_lp:
+            blk = np.zeros(P, np.int32)
+            blk[-1] = 1
+            check(_lib.load().stk_consensus_blocked(ctx._h, _ptr(dev), ns, P, S, blk.ctypes.data, _ptr(out_t),
+                                                    used.ctypes.data))
+        else:
+            check(_lib.load().stk_consensus(ctx._h, _ptr(dev), ns, P, S, _ptr(out_t), used.ctypes.data))
+        return out_t, used.astype(bool)
+    if not isinstance(draws, (list, tuple)) and hasattr(draws, "numpy"):    # a host torch tensor
+        draws = list(draws.numpy())
     X, (P, S) = _stack(draws)
     out = np.empty((P, S))
     used = np.empty(len(draws), np.int32)

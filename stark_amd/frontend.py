@@ -169,3 +169,38 @@ def column_names(family: str, data: dict) -> list:
     if family == "linear":
         cols.append("sigma")
     return cols + ["lp__"]
+
+
+def param_rows(family: str, data: dict) -> "dict[str, list[int]]":
+    """extract() keys in model order (parameters, transformed parameters, lp__) -> their rows
+    in the P x S draw matrix (stark/stark.py:49-56 flattens each key to consecutive rows)."""
+    groups, row = {}, 0
+    for name in column_names(family, data):
+        key = name.split("[")[0]
+        groups.setdefault(key, []).append(row)
+        row += 1
+    return groups
+
+
+def select_pars(family: str, data: dict, pars=None, include: bool = True) -> "list[int] | None":
+    """pystan 2 ``sampling(pars=..., include=...)`` (forwarded by stark/stark.py:48 **kwargs):
+    the rows that ``fit.extract()`` then returns, in its key order.  pars names the parameters
+    to keep (include=True, in the given order) or to drop (include=False, model order kept);
+    lp__ is always returned, last.  Unknown names raise ValueError as pystan does.  None: all
+    rows (no selection)."""
+    if pars is None:
+        return None
+    if isinstance(pars, str):
+        pars = [pars]
+    pars = list(pars)
+    groups = param_rows(family, data)
+    for p in pars:
+        if p not in groups:
+            raise ValueError(f"No parameter {p}")
+    if include:
+        keep = list(dict.fromkeys(p for p in pars if p != "lp__"))
+    else:
+        keep = [k for k in groups if k not in pars and k != "lp__"]
+    keep.append("lp__")
+    return [r for k in keep for r in groups[k]]
+

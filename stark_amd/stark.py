@@ -149,8 +149,7 @@ def sampling_config(family, datas, **kw):
         cfg["init"] = np.concatenate([_unconstrain(family, d, init[c]) for d in datas for c in range(chains)])
     elif init != "random":
         raise ValueError(f"unsupported init {init!r}")
-    for k in ("verbose", "refresh", "sample_file", "diagnostic_file", "check_hmc_diagnostics", "pars",
-              "include", "algorithm"):
+    for k in ("verbose", "refresh", "sample_file", "diagnostic_file", "check_hmc_diagnostics", "algorithm"):
         v = kw.pop(k, None)
         if k == "algorithm" and v not in (None, "NUTS"):
             raise NotImplementedError("only algorithm='NUTS' is supported")
@@ -180,14 +179,22 @@ class Stark:
         self.stan_kwargs = kwargs
 
     # ---- per-partition sampling (stark/stark.py:41-57), batched over partitions
-    def _sample_partitions(self, datas, shard_ids=None, permuted=True, **kwargs):
+    def _sample_partitions(self, datas, shard_ids=None, permuted=True, pars=None, include=True, **kwargs):
         """Run every data dict as one shard of a single GPU model; returns one P x S matrix
         per data dict, rows in extract() order (params, transformed params, lp__), columns in
         ``extract(permuted=True)`` order (``permute_draws``) unless permuted=False.
         shard_ids: global partition index of each data dict (keys the RNG streams, so a
-        partition samples identically on 1 or N GPUs)."""
+        partition samples identically on 1 or N GPUs).  pars / include: pystan 2's parameter
+        selection (``frontend.select_pars``): only those rows (+ lp__) reach the P x S matrix,
+        and so the combine, as in the reference (stark/stark.py:48-56)."""
         if self.family is None:
             raise RuntimeError("call setStanModel() first")
+        rows = [frontend.select_pars(self.family, d, pars, include) for d in datas]   # validates first
+        draws = self._draw_partitions(datas, shard_ids=shard_ids, permuted=permuted, **kwargs)
+        return [d if r is None else np.ascontiguousarray(d[r]) for d, r in zip(draws, rows)]
+
+    def _draw_partitions(self, datas, shard_ids=None, permuted=True, **kwargs):
+        """The GPU run behind _sample_partitions: every extract() row of every partition."""
         shards = [frontend.pack_data(self.family, d) for d in datas]
         cfg = sampling_config(self.family, datas, **kwargs)
         if shard_ids is not None:

@@ -53,7 +53,18 @@ class FakeStanModel:
     def __init__(self, **kwargs):
         self.kwargs = kwargs
 
-    def sampling(self, data, **kw):
+    def sampling(self, data, pars=None, include=True, **kw):
+        """pars / include as pystan 2 applies them to extract(): the named parameters in the
+        given order (include=True) or all others in model order (include=False), lp__ last."""
+        fit = self._sampling(data, **kw)
+        if pars is None:
+            return fit
+        od = fit.extract()
+        pars = [pars] if isinstance(pars, str) else list(pars)
+        keep = [p for p in pars if p != "lp__"] if include else [k for k in od if k not in pars and k != "lp__"]
+        return FakeFit(collections.OrderedDict([(k, od[k]) for k in keep] + [("lp__", od["lp__"])]))
+
+    def _sampling(self, data, **kw):
         J = data["J"]
         S = kw["iter"] // 2 * kw.get("chains", 1)
         seed = int(abs(sum(data["y"]) * 1000 + sum(data["sigma"]))) % (2**32)
@@ -129,6 +140,21 @@ def main():
     combine["nan_f1"] = f1
     combine["nan_f2"] = f2
     combine["nan_out"] = stark.consensus_avg(2)(f1, f2)
+    # rank-deficient sample covariances (S - 1 < P): what the reference's np.linalg.inv does
+    # with them (LAPACK LU: it raises only on an exactly zero pivot)
+    for P, S in ((11, 6), (30, 12)):
+        f1 = spd_draws(rng, P, S)
+        f2 = spd_draws(rng, P, S, 1.3)
+        combine[f"rankdef_P{P}_f1"] = f1
+        combine[f"rankdef_P{P}_f2"] = f2
+        try:
+            red = stark.consensus_avg(2)(f1, f2)
+            final = np.dot(np.linalg.inv(red[0]), red[1])
+            combine[f"rankdef_P{P}_raised"] = np.array(0)
+            combine[f"rankdef_P{P}_final"] = final
+            combine[f"rankdef_P{P}_cond_sumW"] = np.array(np.linalg.cond(red[0]))
+        except np.linalg.LinAlgError:
+            combine[f"rankdef_P{P}_raised"] = np.array(1)
     np.savez_compressed(os.path.join(OUT, "combine_ref.npz"), **combine)
 
     # ---- concatenate_samples (:23-24)
@@ -150,6 +176,10 @@ def main():
     weighted = st.concensusWeight(iter=600)
     naive = st.distribute(n=4, iter=200)
     driver = dict(part0=part0, weighted=weighted, naive=naive)
+    # pystan 2 parameter selection forwarded through **kwargs (stark/stark.py:48): fewer rows reach
+    # the P x S matrix, and so the combine
+    driver["weighted_pars"] = st.concensusWeight(iter=600, pars=["eta", "mu"])
+    driver["naive_exclude"] = st.distribute(n=4, iter=200, pars=["theta", "tau"], include=False)
     # the inputs the fake sampler saw, so tests can rebuild them without the reference
     for k, part in enumerate(rdd.parts):
         fit = FakeStanModel().sampling(prepare(part), iter=600, chains=1)

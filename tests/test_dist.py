@@ -36,6 +36,19 @@ def _worker(rank, world, port, q):
         ok = all(a.shape == shapes[p] and np.array_equal(
             a, np.full(shapes[p], float(p) + 0.5) + np.arange(np.prod(shapes[p])).reshape(shapes[p]))
             for p, a in enumerate(allp))
+        # as_tensor: equal shapes, ONE [partitions, rows, cols] tensor (the bench's device combine input);
+        # local values may be tensors; ragged shapes are refused
+        import torch
+        eq = {p: torch.full((3, 4), float(p)) + torch.arange(12.).reshape(3, 4) for p in mine}
+        t = sdist.all_gather_partitions(eq, len(shapes), as_tensor=True)
+        ok = ok and tuple(t.shape) == (5, 3, 4) and t.dtype == torch.float64 and all(
+            torch.equal(t[p], torch.full((3, 4), float(p), dtype=torch.float64) + torch.arange(12.).reshape(3, 4))
+            for p in range(5))
+        try:
+            sdist.all_gather_partitions(local, len(shapes), as_tensor=True)
+            ok = False
+        except ValueError:
+            pass
         # driver with a fake sampler: naive mode across ranks
         import pytest as _pt  # noqa: F401
         from test_host import _fake_stark

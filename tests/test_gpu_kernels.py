@@ -120,6 +120,66 @@ def test_combine_nan_guard(ctx, golden):
     np.testing.assert_allclose(comb, g["nan_f2"], rtol=1e-9, atol=1e-9)   # only shard 2 left
 
 
+def test_combine_public_solve_is_a_general_inverse(ctx):
+    """stk_consensus_solve takes the caller's sum W: any invertible matrix, inverted as
+    np.linalg.inv does (partial pivoting; stark/stark.py:67-70) -- also a non-symmetric one and a
+    symmetric indefinite one; an exactly singular one raises LinAlgError as numpy does."""
+    from stark_amd import engine
+    from stark_amd._lib import LinAlgError
+    rng = np.random.default_rng(5)
+    for P in (11, 102, 140):
+        swt = rng.normal(size=(P, 64))
+        ns = rng.normal(size=(P, P)) + 3 * np.eye(P)                    # not symmetric
+        ind = rng.normal(size=(P, P))
+        ind = ind + ind.T                                              # symmetric indefinite
+        for M in (ns, ind):
+            ref = np.linalg.inv(M) @ swt
+            out = engine.consensus_solve(M, swt, ctx)
+            np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-11 * np.abs(ref).max() * np.linalg.cond(M))
+    sing = np.ones((5, 5))
+    with pytest.raises(np.linalg.LinAlgError):
+        np.linalg.inv(sing)
+    with pytest.raises(LinAlgError):
+        engine.consensus_solve(sing, rng.normal(size=(5, 8)), ctx)
+
+
+@pytest.mark.parametrize("P", [11, 30])
+def test_combine_rank_deficient_covariance(ctx, golden, P):
+    """S - 1 < P draws: each sample covariance is singular.  The reference's np.linalg.inv does
+    not raise on it (LAPACK LU meets no exactly zero pivot) and returns an 'inverse' made of
+    rounding noise (tests/golden/make_golden.py records it); the GPU combine, which inverts
+    covariances by diagonal pivoting, reports the singular covariance as LinAlgError -- the
+    documented deviation (include/stark_hip.h)."""
+    from stark_amd import engine
+    from stark_amd._lib import LinAlgError
+    g = golden("combine_ref.npz")
+    f1, f2 = g[f"rankdef_P{P}_f1"], g[f"rankdef_P{P}_f2"]
+    assert f1.shape[1] - 1 < P and int(g[f"rankdef_P{P}_raised"]) == 0
+    with pytest.raises(LinAlgError):
+        engine.consensus([f1, f2], ctx)
+
+
+def test_combine_device_draws_match_host(ctx):
+    """Device-resident draws (a [shards, P, S] cuda tensor, as dist.all_gather_partitions(...,
+    as_tensor=True) returns them) combine where they lie, bit-identical to the host-buffer path."""
+    import torch
+    from stark_amd import engine
+    rng = np.random.default_rng(9)
+    P, S, ns = 40, 500, 8
+    draws = []
+    for _ in range(ns):
+        A = rng.normal(size=(P, P)) / np.sqrt(P)
+        draws.append(rng.normal(size=(P, 1)) + np.linalg.cholesky(A @ A.T + 0.5 * np.eye(P)) @ rng.normal(size=(P, S)))
+    host, used_h = engine.consensus(draws, ctx, separate_lp=True)
+    dev_in = torch.as_tensor(np.stack(draws), device=f"cuda:{ctx.device}")
+    out, used = engine.consensus(dev_in, ctx, separate_lp=True)
+    assert out.is_cuda and tuple(out.shape) == (P, S)
+    np.testing.assert_array_equal(out.cpu().numpy(), host)
+    assert list(used) == list(used_h)
+    out2, _ = engine.consensus([t for t in dev_in], ctx)
+    np.testing.assert_array_equal(out2.cpu().numpy(), engine.consensus(draws, ctx)[0])
+
+
 @pytest.mark.parametrize("S", [1, 3, 8])
 def test_combine_general_shards(ctx, orc, S):
     from stark_amd import engine

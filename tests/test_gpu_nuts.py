@@ -98,14 +98,16 @@ def test_adaptive_run_tracks_oracle(ctx, orc, nw, jitter):
     res.close()
 
 
-def _packed_schools_run(ctx=None):
+def _packed_schools_run(ctx=None, chains_per_wave=0):
     """10 chains of 8 schools (D = 10): 3 waves of the fused kernel at 4 chains per wave (the
-    last one partly empty), warmup with adaptation + draws; returns unconstrained draws and stats."""
+    last one partly empty; chains_per_wave caps the packing), warmup with adaptation + draws;
+    returns unconstrained draws and stats."""
     from oracle import oracle as orc
     from stark_amd import engine
     ctx = ctx or engine.Context(0)
     m = engine.Model(ctx, "schools", [{"y": orc.SCHOOLS_Y, "sigma": orc.SCHOOLS_SIGMA}])
-    s = m.sampler(num_warmup=30, num_samples=25, chains=10, seed=91, save_warmup=True)
+    s = m.sampler(num_warmup=30, num_samples=25, chains=10, seed=91, save_warmup=True,
+                  chains_per_wave=chains_per_wave)
     s.run()
     uq, st = s.unconstrained(0), s.draws(0)[1]
     s.close()
@@ -113,22 +115,15 @@ def _packed_schools_run(ctx=None):
     return uq, st
 
 
-def test_packed_schools_chains_bitwise_equal_unpacked(ctx, orc, tmp_path):
+def test_packed_schools_chains_bitwise_equal_unpacked(ctx, orc):
     """Packing 4 chains per wave (16 lanes each; segmented DPP sums) changes no bit: the same
-    run with one chain per wave (STARK_FUSED_CPW=1, a separate process: the choice is read once)
-    gives identical draws and stats; and every chain starts on the recursive Stan twin's path."""
-    import subprocess
-    import sys
-    from conftest import ROOT
+    run with one and with two chains per wave (stk_config.chains_per_wave) gives identical draws
+    and stats; and every chain starts on the recursive Stan twin's path."""
     uq, st = _packed_schools_run(ctx)
-    out = tmp_path / "cpw1.npz"
-    code = ("import sys, numpy as np; sys.path[:0] = [%r, %r]; from test_gpu_nuts import _packed_schools_run; "
-            "u, s = _packed_schools_run(); np.savez(%r, u=u, s=s)" % (ROOT, os.path.join(ROOT, "tests"), str(out)))
-    subprocess.run([sys.executable, "-c", code], check=True, timeout=240,
-                   env=dict(os.environ, STARK_FUSED_CPW="1"))
-    ref = np.load(out)
-    np.testing.assert_array_equal(uq, ref["u"])
-    np.testing.assert_array_equal(st, ref["s"])
+    for cpw in (1, 2):
+        u1, s1 = _packed_schools_run(ctx, chains_per_wave=cpw)
+        np.testing.assert_array_equal(uq, u1)
+        np.testing.assert_array_equal(st, s1)
     om = orc.Model(orc.FAM_SCHOOLS, y=orc.SCHOOLS_Y, sigma=orc.SCHOOLS_SIGMA)
     for c in range(uq.shape[0]):
         o = om.run_chain(num_warmup=30, num_samples=25, seed=91, gid=c)
@@ -267,6 +262,11 @@ def test_driver_weighted_matches_reference(ctx, golden, monkeypatch):
     g = golden("driver_ref.npz")
     out = st.concensusWeight(iter=600)
     ref = g["weighted"]
+    np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-10 * np.abs(ref).max())
+    # with pystan 2's pars= selection the combine runs on the selected rows only (stark/stark.py:48-56)
+    out = st.concensusWeight(iter=600, pars=["eta", "mu"])
+    ref = g["weighted_pars"]
+    assert out.shape == ref.shape == (6, 300)
     np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-10 * np.abs(ref).max())
 
 

@@ -33,15 +33,15 @@ def test_library_exports_every_header_symbol():
     # struct layouts must match the C header: compile a probe with gcc
     import subprocess, tempfile
     src = ('#include <stdio.h>\n#include <stddef.h>\n#include "stark_hip.h"\n'
-           'int main(){printf("%zu %zu %zu %zu %zu", sizeof(stk_config), sizeof(stk_shard), sizeof(stk_run_info),'
-           ' offsetof(stk_config, seed), offsetof(stk_config, shard_ids));return 0;}')
+           'int main(){printf("%zu %zu %zu %zu %zu %zu", sizeof(stk_config), sizeof(stk_shard), sizeof(stk_run_info),'
+           ' offsetof(stk_config, seed), offsetof(stk_config, shard_ids), offsetof(stk_config, chains_per_wave));return 0;}')
     with tempfile.TemporaryDirectory() as d:
         open(os.path.join(d, "p.c"), "w").write(src)
         subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", os.path.join(d, "p"), os.path.join(d, "p.c")],
                        check=True)
         got = [int(v) for v in subprocess.run([os.path.join(d, "p")], capture_output=True, text=True).stdout.split()]
     assert got == [ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.Shard), ctypes.sizeof(_lib.RunInfo),
-                   _lib.Config.seed.offset, _lib.Config.shard_ids.offset]
+                   _lib.Config.seed.offset, _lib.Config.shard_ids.offset, _lib.Config.chains_per_wave.offset]
 
 
 def test_no_device_fails_loudly():
@@ -147,7 +147,8 @@ def _fake_stark(monkeypatch):
     def fake(self, datas, **kw):
         return [S._extract_to_matrix(_fake_extract(d, kw["iter"], kw.get("chains", 1))) for d in datas]
 
-    monkeypatch.setattr(S.Stark, "_sample_partitions", fake)
+    # below the pars / include row selection of _sample_partitions, which runs for real
+    monkeypatch.setattr(S.Stark, "_draw_partitions", fake)
     sc = LocalContext()
     school = list(zip([28, 8, -3, 7, -1, 1, 18, 12], [15, 10, 16, 11, 9, 11, 10, 18]))
     st = S.Stark(sc, sc.parallelize(school, 2), prepare_school_data)
@@ -171,6 +172,25 @@ def test_driver_distribute_reference_union(golden, monkeypatch):
     np.testing.assert_array_equal(out, g["naive"])
     intent = st.distribute(n=4, iter=200)
     assert intent.shape == (4 * 19, 100)
+
+
+def test_driver_pars_include_matches_reference(golden, monkeypatch):
+    """pystan 2 sampling(pars=, include=) forwarded through the driver's **kwargs
+    (stark/stark.py:48): only the selected parameters (+ lp__, last) reach the P x S matrix --
+    against the reference driver run with a fake StanModel that honours them
+    (tests/golden/make_golden.py)."""
+    st = _fake_stark(monkeypatch)
+    g = golden("driver_ref.npz")
+    out = st.distribute(n=4, iter=200, reference_union=True, pars=["theta", "tau"], include=False)
+    np.testing.assert_array_equal(out, g["naive_exclude"])
+    w = st._mcmc(prepare_school_data, iter=600, chains=1, n_jobs=1, pars=["eta", "mu"])
+    part0 = w(iter(list(zip([28, 8, -3, 7], [15, 10, 16, 11]))))[0]
+    assert part0.shape == (6, 300)          # eta[1..4], mu, lp__
+    with pytest.raises(ValueError, match="No parameter"):
+        st.distribute(n=2, iter=200, pars=["nope"])
+    from stark_amd import frontend
+    assert frontend.select_pars("logistic", {"K": 3}, ["beta"]) == [1, 2, 3, 4]
+    assert frontend.select_pars("linear", {"K": 2}, ["beta"], include=False) == [0, 3, 4]
 
 
 # ---------------------------------------------------------------- diagnostics

@@ -39,11 +39,13 @@ def main():
     p.add_argument("--warmup", type=int, default=1000)
     p.add_argument("--samples", type=int, default=1000)
     p.add_argument("--seed", type=int, default=7)
+    p.add_argument("--chains-per-wave", type=int, default=0, help="fused kernel packing cap (0: 4 chains per wave)")
     a = p.parse_args()
     from stark_amd import diagnostics, engine
     ctx = engine.Context(0)
     m = engine.Model(ctx, "schools", [{"y": np.array(Y), "sigma": np.array(SIGMA)}])
-    s = m.sampler(num_warmup=a.warmup, num_samples=a.samples, chains=a.chains, seed=a.seed)
+    s = m.sampler(num_warmup=a.warmup, num_samples=a.samples, chains=a.chains, seed=a.seed,
+                  chains_per_wave=a.chains_per_wave)
     ctx.sync()
     t0 = time.perf_counter()
     s.run(a.warmup)
@@ -75,7 +77,7 @@ def main():
                      "achieved": (i2["grad_evals"] - i1["grad_evals"]) / samp * FLOPS_PER_GRAD(len(Y)) / 1e12,
                      "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                      "flops_per_grad": FLOPS_PER_GRAD(len(Y))},
-        "chains_per_wave": int(os.environ.get("STARK_FUSED_CPW", "4")),
+        "chains_per_wave": a.chains_per_wave or 4,
     }
     line["roofline"]["frac"] = line["roofline"]["achieved"] / FP64_PEAK_TFS
     print(json.dumps(line), flush=True)

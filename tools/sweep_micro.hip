@@ -3,11 +3,12 @@
 //            sweep's chunking), 8 loads in flight per thread: the HBM read ceiling;
 //   skeleton v2's tile pipeline (register prefetch one tile ahead, LDS staging, 4 barriers
 //            per tile) with the arithmetic removed;
-//   sweep    the product kernel (stk_launch_sweep, variant per STARK_SWEEP / shape), all
+//   sweep    the product kernel (stk_launch_sweep, variant per STARK_SWEEP=1|2|3 / shape), all
 //            shards in one launch.
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/sweep_micro.hip -o tools/_bin/sweep_micro
 // Run:   tools/_bin/sweep_micro [rows_per_shard] [shards] [d] [reps]
 #include "../stark_amd/csrc/sweep.hip"
+#include "sweep_variants.hip"
 #include "../stark_amd/csrc/datagen.hip"
 #include <stdarg.h>
 #include <stdio.h>
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(512) void k_skel3(SweepArgs A, int NB, double* sink
 }  // namespace stk
 
 int main(int argc, char** argv) {
+  if (const char* e = getenv("STARK_SWEEP")) stk_sweep_force_variant = atoi(e);   // this tool only
   const int64_t rows = argc > 1 ? atoll(argv[1]) : 12500000;
   const int nsh = argc > 2 ? atoi(argv[2]) : 4;
   const int d = argc > 3 ? atoi(argv[3]) : 100;
