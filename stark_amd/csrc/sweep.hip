@@ -770,6 +770,83 @@ __device__ __forceinline__ void softplus_tab(double ntt, const double* tab, doub
   *w = e * ri;
 }
 
+// Logistic residual v2 (k_sweepe): Stan's bernoulli_logit term lt and its derivative dv for
+// one (row, chain) from ONE exp and ONE log1p of a = |t|, t = (2y - 1) eta:
+//   e = exp(-a)                 x = -a = n ln2/128 + r, |r| <= ln2/256; e^r by degree 4 (rel. error
+//                               1.2e-15), times T_{n mod 128} = 2^{(n mod 128)/128} from LDS, times
+//                               2^{n div 128} added to the exponent field with an integer add (a is
+//                               clamped to 700, so the result stays a normal number);
+//                               n = rint(x 128/ln2) comes from the low word of fma(x, 128/ln2, 1.5 2^52);
+//   lg = log1p(e)               j = rint(128 e) (the same fma trick), c_j = 128/(128 + j),
+//                               d_j = j/(128 + j), l_j = log(1 + j/128): rl = e c_j - d_j (one fma,
+//                               |rl| <= 1/256, exact for j = 0 so small e keeps its relative accuracy,
+//                               and 1 + e is never formed), lg = l_j + rl q(rl), q of degree 5;
+//   ri = 1/(1 + e)              v_rcp_f64 + one Newton step;  w = e ri.
+// Then lt = min(t, 0) - lg and dv/sgn = (t < 0 ? ri : w), with Stan's lower cutoff t < -20 ->
+// (lt, dv/sgn) = (t, 1) applied as a select (NaN takes that branch, so a NaN eta stays NaN).
+// Stan's upper cutoff (t > 20: -exp(-t), exp(-t)) differs from the smooth expressions by
+// <= e^2 <= 4.3e-18 and needs no branch.  t and dv's sign come from an XOR of the sign bit
+// (ymask = 0x80000000 for y = 0).  About 30 f64 instructions per (row, chain) against ~50 for
+// softplus_tab (fp64 VALU and fp64 MFMA share one pipe on gfx950).
+constexpr int LG_TAB = 128 + 4 * 129;     // doubles: T[128], then [c_j, d_j, l_j, 0] for j = 0..128
+__device__ void logit_tables_init(double* tab) {
+  for (int i = threadIdx.x; i < LG_TAB; i += blockDim.x) {
+    double v;
+    if (i < 128) {
+      v = exp2((double)i / 128.0);
+    } else {
+      const int j = (i - 128) >> 2, f = (i - 128) & 3;
+      v = f == 0 ? 128.0 / (128 + j) : (f == 1 ? (double)j / (128 + j) : (f == 2 ? log1p((double)j / 128.0) : 0.0));
+    }
+    tab[i] = v;
+  }
+}
+
+// 64-bit select as an integer bit blend (v_bfi_b32 x 2): a C++ conditional here lets the
+// compiler sink a whole arm's arithmetic into an exec-masked branch, which serialises the
+// four (row, chain) pairs of a lane instead of interleaving them
+__device__ __forceinline__ double blend(uint32_t m, double a, double b) {   // m = ~0u: a, 0: b
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const uint64_t mm = ((uint64_t)m << 32) | m;
+  return __builtin_bit_cast(double, (ua & mm) | (ub & ~mm));
+}
+
+__device__ __forceinline__ void logit_resid(double eta, uint32_t ymask, const double* tab, double& lt, double& dv) {
+  constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
+  constexpr double INV_L = 184.6649652337873;            // 128 / ln 2
+  constexpr double L_HI = 0.005415212348452769;          // ln2/128 rounded to 32 significant bits: n L_HI exact
+  constexpr double L_LO = -3.2819649005320973e-13;       // ln2/128 - L_HI
+  const double t = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, eta) ^ ((uint64_t)ymask << 32));
+  const double a = fabs(t);
+  // n = rint(-a 128/ln2) from the low word, clamped at -128 * 1010 (a ~ 700): past it e is a
+  // positive number below 1e-290 instead of exp(-a) (|lt|, |dv| error < 1e-290)
+  const double sn = fma(-a, INV_L, MAGIC);
+  const int ni = max((int)(uint32_t)__builtin_bit_cast(uint64_t, sn), -128 * 1010);
+  const double n = (double)ni;
+  double r = fma(-n, L_HI, -a);
+  r = fma(-n, L_LO, r);
+  const double p = fma(fma(fma(fma(1.0 / 24.0, r, 1.0 / 6.0), r, 0.5), r, 1.0), r, 1.0);
+  const double tp = tab[ni & 127] * p;
+  const double e = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, tp) + ((uint64_t)(int64_t)(ni >> 7) << 52));
+  const double sj = fma(e, 128.0, MAGIC);
+  const int j = (int)(uint32_t)__builtin_bit_cast(uint64_t, sj);
+  const double* cj = tab + 128 + 4 * j;
+  const dbl2 cd = *reinterpret_cast<const dbl2*>(cj);
+  const double rl = fma(e, cd.x, -cd.y);
+  const double q = fma(fma(fma(fma(fma(-1.0 / 6.0, rl, 0.2), rl, -0.25), rl, 1.0 / 3.0), rl, -0.5), rl, 1.0);
+  const double lg = fma(rl, q, cj[2]);
+  const double u = 1.0 + e;
+  double ri = __builtin_amdgcn_rcp(u);
+  ri = fma(ri, fma(-u, ri, 1.0), ri);
+  const double w = e * ri;
+  const uint32_t neg = (uint32_t)((int32_t)(__builtin_bit_cast(uint64_t, t) >> 32) >> 31);   // ~0u when t < 0 (or -0)
+  const uint32_t lo = (t >= -20.0) ? 0u : ~0u;                                                 // Stan's cutoff; NaN too
+  const double lts = blend(neg, t, 0.0) - lg;                                                  // min(t, 0) - lg
+  lt = blend(lo, t, lts);
+  const double dvp = blend(lo, 1.0, blend(neg, ri, w));
+  dv = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, dvp) ^ ((uint64_t)ymask << 32));
+}
+
 // ABL (micro-benchmark ablations only): bit 0 linear residual stand-in, bit 1 no backward,
 // bit 2 no forward.  KFS/JTS: compile-time KF / JT for the BASELINE shapes (0 = runtime).
 template <int FAM, int KFS = 0, int JTS = 0, int ABL = 0, int MINB = SM_MINB, bool VREM = false>
@@ -800,7 +877,7 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
   char* const ring = reinterpret_cast<char*>(lds) + (size_t)w * NB * SS;
   double* const sptab = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * NB * SS);
   if constexpr (FAM == STK_LOGREG) {
-    softplus_tables_init(sptab);
+    logit_tables_init(sptab);
     __syncthreads();
   }
 
@@ -889,13 +966,7 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
       } else if constexpr (FAM == STK_LOGREG) {
         // Stan's bernoulli_logit: ntt > 20 -> -exp(-ntt); ntt < -20 -> ntt; else -log1p(exp(-ntt))
         const int32_t yv = *reinterpret_cast<const int32_t*>(sl + SBX + row * 4);
-        const double sgn = 2.0 * yv - 1.0;
-        const double ntt = sgn * eta;
-        double e, lm, wt;
-        softplus_tab(ntt, sptab, &e, &lm, &wt);
-        const bool hi = ntt > 20.0, lo = ntt < -20.0;
-        lt = hi ? -e : (lo ? ntt : -lm);
-        dv = sgn * (hi ? e : (lo ? 1.0 : wt));
+        logit_resid(eta, yv == 0 ? 0x80000000u : 0u, sptab, lt, dv);
       } else {
         const double yv = *reinterpret_cast<const double*>(sl + SBX + row * 8);
         const double z = (yv - eta) * inv_s;
@@ -993,7 +1064,12 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
 #ifndef SE_BPAD
 #define SE_BPAD 2
 #endif
-template <int FAM, int KF, int JT, int ABL = 0>
+// RV: logistic residual version, 2 = logit_resid (alpha folded into the forward's accumulator
+// init, sign flips by XOR; the product), 1 = softplus_tab (kept for A/B in tools/sweep_micro.hip).
+// ER: early release -- the forward's A operands (25 values per lane) are read into registers with
+// everything else the sub-tile needs BEFORE the forward, so the slot is refilled while the
+// forward, the residual and the backward all run (ER = 0: after the forward, round 2).
+template <int FAM, int KF, int JT, int ABL = 0, int RV = 2, int NACC = SE_NACC, int ER = 1>
 __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   constexpr int C = SM_C, NW = SM_W, JTV = JT - 1, KP = 4 * KF, KB = KP + SE_BPAD;
   const int shard = A.shard0 + blockIdx.x / A.G;
@@ -1018,7 +1094,11 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   char* const slot = reinterpret_cast<char*>(lds) + (size_t)w * SS;
   double* const bimg = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);  // [16][KB]
   double* const sptab = bimg + C * KB;
-  if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
+  // ER: the 4 remainder columns (16 rows x 4) of the wave's sub-tile, kept past the slot's release
+  double* const xst = sptab + LG_TAB + w * 64;
+  constexpr bool R2 = FAM == STK_LOGREG && RV == 2;
+  if constexpr (R2) logit_tables_init(sptab);
+  else if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
   const double* qs = A.q + (size_t)shard * C * A.Dp;
   for (int i = tid; i < C * KP; i += NW * 64) {
     const int c = i / KP, col = i % KP;
@@ -1059,18 +1139,20 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
     __builtin_amdgcn_s_waitcnt(0xF70);                   // vmcnt(0): sub-tile k landed
     __builtin_amdgcn_sched_barrier(0);
     const int rv = std::min(SM_R, nrows - SM_R * (w + NW * k));
-    // ---- forward
-    dbl4 ea[SE_NACC];
+    // ---- forward (ER: operands first, MFMAs after the slot is released)
+    dbl4 ea[NACC];
 #pragma unroll
-    for (int i = 0; i < SE_NACC; ++i) ea[i] = dbl4{0.0, 0.0, 0.0, 0.0};
-    if constexpr (!(ABL & 4)) {
-      const double* xrow = xs + lr * d;
+    for (int i = 0; i < NACC; ++i) ea[i] = dbl4{0.0, 0.0, 0.0, 0.0};
+    if constexpr (R2) ea[0] = dbl4{alpha, alpha, alpha, alpha};     // D layout: lane holds chain lr
+    double fa[ER ? KF : 1];
+    const double* xrow = xs + lr * d;
+    if constexpr (ER) {
 #pragma unroll
-      for (int s = 0; s < KF; ++s) ea[s % SE_NACC] = mfma_f64(xrow[std::min(lh * KF + s, d - 1)], brow[s], ea[s % SE_NACC]);
+      for (int s = 0; s < KF; ++s) fa[s] = xrow[std::min(lh * KF + s, d - 1)];
+    } else if constexpr (!(ABL & 4)) {
+#pragma unroll
+      for (int s = 0; s < KF; ++s) ea[s % NACC] = mfma_f64(xrow[std::min(lh * KF + s, d - 1)], brow[s], ea[s % NACC]);
     }
-    dbl4 e0 = ea[0], e1 = ea[1];
-#pragma unroll
-    for (int i = 2; i < SE_NACC; ++i) { if (i & 1) e1 += ea[i]; else e0 += ea[i]; }
     // ---- everything the rest of the sub-tile needs from the slot, into registers
     double xa[4][JTV];
 #pragma unroll
@@ -1079,22 +1161,60 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
       for (int t = 0; t < JTV; ++t) xa[s][t] = xs[(lh + 4 * s) * d + 16 * t + lr];
     dbl2 xv[4][2];
     double yv[4];
+    uint32_t ym[4];
+    if constexpr (ER) xst[lane] = xs[(lane >> 2) * d + 16 * JTV + (lane & 3)];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const dbl2* p = reinterpret_cast<const dbl2*>(xs + (lh + 4 * i) * d + 16 * JTV);
-      xv[i][0] = p[0];
-      xv[i][1] = p[1];
-      yv[i] = (FAM == STK_LOGREG) ? (double)*reinterpret_cast<const int32_t*>(slot + SBX + (lh + 4 * i) * 4)
-                                  : *reinterpret_cast<const double*>(slot + SBX + (lh + 4 * i) * 8);
+      if constexpr (!ER) {
+        const dbl2* p = reinterpret_cast<const dbl2*>(xs + (lh + 4 * i) * d + 16 * JTV);
+        xv[i][0] = p[0];
+        xv[i][1] = p[1];
+      }
+      if constexpr (R2) {
+        ym[i] = (uint32_t)(*reinterpret_cast<const int32_t*>(slot + SBX + (lh + 4 * i) * 4) == 0) << 31;
+      } else {
+        yv[i] = (FAM == STK_LOGREG) ? (double)*reinterpret_cast<const int32_t*>(slot + SBX + (lh + 4 * i) * 4)
+                                    : *reinterpret_cast<const double*>(slot + SBX + (lh + 4 * i) * 8);
+      }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): the slot is free
     __builtin_amdgcn_sched_barrier(0);
     if (k + 1 < mine) issue(k + 1);
     __builtin_amdgcn_sched_barrier(0);
-    const dbl4 eta4 = e0 + e1;
+    if constexpr (ER && !(ABL & 4)) {
+#pragma unroll
+      for (int s = 0; s < KF; ++s) ea[s % NACC] = mfma_f64(fa[s], brow[s], ea[s % NACC]);
+    }
+    dbl4 e0 = ea[0], e1 = {0.0, 0.0, 0.0, 0.0};
+    if constexpr (NACC > 1) e1 = ea[1];
+#pragma unroll
+    for (int i = 2; i < NACC; ++i) { if (i & 1) e1 += ea[i]; else e0 += ea[i]; }
+    const dbl4 eta4 = NACC > 1 ? e0 + e1 : e0;
 
     // ---- residual
     double de[4];
+    if constexpr (R2 && !(ABL & 1)) {
+      if (rv == SM_R) {                                  // full sub-tile (all but a chunk's last): no masks
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double lt;
+          logit_resid(eta4[i], ym[i], sptab, lt, de[i]);
+          lpa += lt;
+          gaa += de[i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool valid = lh + 4 * i < rv;
+          double lt, dv;
+          logit_resid(eta4[i], ym[i], sptab, lt, dv);
+          dv = valid ? dv : 0.0;
+          lpa += valid ? lt : 0.0;
+          gaa += dv;
+          de[i] = dv;
+        }
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool valid = lh + 4 * i < rv;
@@ -1129,6 +1249,11 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
         for (int t = 0; t < JTV; ++t) gacc[t] = mfma_f64(xa[s][t], de[s], gacc[t]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        if constexpr (ER) {
+          const dbl2* p = reinterpret_cast<const dbl2*>(xst + (lh + 4 * i) * 4);
+          xv[i][0] = p[0];
+          xv[i][1] = p[1];
+        }
         gv[0] = fma(xv[i][0].x, de[i], gv[0]);
         gv[1] = fma(xv[i][0].y, de[i], gv[1]);
         gv[2] = fma(xv[i][1].x, de[i], gv[2]);
@@ -1275,7 +1400,7 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
   extern __shared__ __attribute__((aligned(16))) double lds[];
   char* const stg = reinterpret_cast<char*>(lds);                 // NS stages of STG bytes
   double* const sptab = reinterpret_cast<double*>(stg + NS * STG);
-  if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
+  if constexpr (FAM == STK_LOGREG) logit_tables_init(sptab);
 
   // per-lane chain constants: chain 16 ct + lr, ct = 2 wc + c2
   const double* qb = A.q + (size_t)shard * G5_C * A.Dp;
@@ -1375,12 +1500,7 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
           const double eta = *eslot(e) + al;
           double dv, lt;
           if constexpr (FAM == STK_LOGREG) {
-            const double sgn = 2.0 * yv - 1.0, ntt = sgn * eta;
-            double ex, lm, wt;
-            softplus_tab(ntt, sptab, &ex, &lm, &wt);
-            const bool hi = ntt > 20.0, lo = ntt < -20.0;
-            lt = hi ? -ex : (lo ? ntt : -lm);
-            dv = sgn * (hi ? ex : (lo ? 1.0 : wt));
+            logit_resid(eta, yv == 0.0 ? 0x80000000u : 0u, sptab, lt, dv);
           } else {
             const double z = (yv - eta) * isg;
             lt = z * z;
@@ -1606,7 +1726,7 @@ static int sweep3_nb(int d, int C) {
 // Ring depth of v4 (C = 16): slots of 16 rows per wave that fit SM_MINB blocks per CU, at most 6,
 // DMAs in flight <= 63 (d = 100: NB = 1, two blocks per CU).
 static int sweepm_nb(int d, int minb = SM_MINB) {
-  int nb = std::min(6, (160 * 1024 / minb - SP_TAB * 8) / (SM_W * sweepm_slot_bytes(d)));
+  int nb = std::min(6, (160 * 1024 / minb - LG_TAB * 8) / (SM_W * sweepm_slot_bytes(d)));
   const int pt = ((SM_R * d * 8 + 1023) >> 10) + 1;
   while (nb > 2 && (nb - 2) * pt > 63) --nb;
   return nb;
@@ -1635,7 +1755,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *T = G5_TR;
     *LD = 0;
     *G = (int)g;
-    *lds_bytes = G5_FS * g5_fstage_bytes() + SP_TAB * sizeof(double);
+    *lds_bytes = G5_FS * g5_fstage_bytes() + LG_TAB * sizeof(double);
     return;
   }
   if (var == 4) {
@@ -1648,8 +1768,8 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *LD = nb;
     *G = (int)g;
     const int JT = (d + 15) / 16;
-    size_t ring = (size_t)SM_W * nb * sweepm_slot_bytes(d) + SP_TAB * sizeof(double);
-    if (d == 100) ring = (size_t)SM_W * sweepm_slot_bytes(d) + (16 * (100 + SE_BPAD) + SP_TAB) * sizeof(double);   // v4e
+    size_t ring = (size_t)SM_W * nb * sweepm_slot_bytes(d) + LG_TAB * sizeof(double);
+    if (d == 100) ring = (size_t)SM_W * sweepm_slot_bytes(d) + (16 * (100 + SE_BPAD) + std::max(SP_TAB, LG_TAB) + SM_W * 64) * sizeof(double);   // v4e
     const size_t red = ((size_t)SM_W * JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * sizeof(double);
     *lds_bytes = std::max(ring, red);
     return;

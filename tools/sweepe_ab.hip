@@ -1,0 +1,137 @@
+// A/B timing of k_sweepe variants at the bench geometry (BASELINE configs[3]: 8 shards x 1.25e7
+// rows, d = 100, 16 chains; 80.4 GB per sweep), interleaved rounds so box drift hits every arm:
+//   e2er    the product kernel: logit_resid (RV = 2), early slot release (ER = 1)
+//   e2      logit_resid, the slot released after the forward (ER = 0)
+//   e1      the round-2 kernel: softplus_tab (RV = 1), ER = 0
+//   e2er-fwd / -bwd / -all   ablations (no forward / no backward / no arithmetic)
+// and a parity check: lp / gradient of e2 and e1 vs e2er after the chunk reduction (relative).
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/sweepe_ab.hip -o tools/_bin/sweepe_ab
+// Run:   tools/_bin/sweepe_ab [rows_per_shard] [shards] [rounds] [reps]
+#include "../stark_amd/csrc/sweep.hip"
+#include "../stark_amd/csrc/datagen.hip"
+#include <stdarg.h>
+#include <stdio.h>
+#include <vector>
+
+void stk_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfprintf(stderr, fmt, ap);
+  va_end(ap);
+  fputc('\n', stderr);
+}
+
+#define CK(x)                                                                             \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(1);                                                                            \
+    }                                                                                     \
+  } while (0)
+
+using namespace stk;
+
+int main(int argc, char** argv) {
+  const int64_t rows = argc > 1 ? atoll(argv[1]) : 12500000;
+  const int nsh = argc > 2 ? atoi(argv[2]) : 8;
+  const int rounds = argc > 3 ? atoi(argv[3]) : 3;
+  const int reps = argc > 4 ? atoi(argv[4]) : 10;
+  const int d = 100, C = 16, Dp = (d + 1 + 7) / 8 * 8;
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  std::vector<ShardDev> sh(nsh);
+  std::vector<double> beta(d);
+  for (int j = 0; j < d; ++j) beta[j] = ((j * 37) % 19 - 9) / (9.0 * sqrt((double)d));
+  double* beta_d;
+  CK(hipMalloc(&beta_d, sizeof(double) * d));
+  CK(hipMemcpy(beta_d, beta.data(), sizeof(double) * d, hipMemcpyHostToDevice));
+  for (int s = 0; s < nsh; ++s) {
+    double* X;
+    int32_t* y;
+    CK(hipMalloc(&X, sizeof(double) * rows * d));
+    CK(hipMalloc(&y, sizeof(int32_t) * rows));
+    CK(stk_launch_gen_shard(X, nullptr, y, rows, d, s * rows, 20240, 0.0, beta_d, 1.0, STK_LOGREG, st));
+    sh[s] = ShardDev{X, nullptr, y, nullptr, rows, d, d + 1, d + 2};
+  }
+  ShardDev* sh_d;
+  CK(hipMalloc(&sh_d, sizeof(ShardDev) * nsh));
+  CK(hipMemcpy(sh_d, sh.data(), sizeof(ShardDev) * nsh, hipMemcpyHostToDevice));
+  std::vector<double> qh((size_t)nsh * C * Dp, 0.0);
+  for (int g = 0; g < nsh * C; ++g) {
+    qh[(size_t)g * Dp] = 0.05 * ((g % 5) - 2);                      // alpha
+    for (int j = 0; j < d; ++j) qh[(size_t)g * Dp + 1 + j] = beta[j] * (0.9 + 0.01 * g);
+  }
+  double *q, *partial, *lp, *grad;
+  CK(hipMalloc(&q, sizeof(double) * qh.size()));
+  CK(hipMemcpy(q, qh.data(), sizeof(double) * qh.size(), hipMemcpyHostToDevice));
+  int T, LD, G;
+  size_t lds;
+  stk_sweep_geometry(rows, d, &T, &LD, &G, &lds, C);
+  CK(hipMalloc(&partial, sizeof(double) * (size_t)nsh * G * C * (d + 2)));
+  CK(hipMalloc(&lp, sizeof(double) * nsh * C));
+  CK(hipMalloc(&grad, sizeof(double) * nsh * C * Dp));
+  CK(hipStreamSynchronize(st));
+  const double bytes = (double)nsh * rows * (8.0 * d + 4.0);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  SweepArgs A{sh_d, q, partial, nullptr, 0, C, Dp, G, LD, d + 2, 0, G, nullptr};
+  printf("rows/shard %lld shards %d d %d C %d: G %d lds %zu, %.1f GB per sweep\n", (long long)rows, nsh, d, C, G, lds,
+         bytes / 1e9);
+  struct Arm { const char* name; const void* kern; std::vector<float> ms; };
+  std::vector<Arm> arms = {
+      {"e2er", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 1>, {}},
+      {"e2", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 0>, {}},
+      {"e1", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 1, 2, 0>, {}},
+      {"e2er-fwd", (const void*)k_sweepe<STK_LOGREG, 25, 7, 4, 2, 2, 1>, {}},
+      {"e2er-bwd", (const void*)k_sweepe<STK_LOGREG, 25, 7, 2, 2, 2, 1>, {}},
+      {"e2er-all", (const void*)k_sweepe<STK_LOGREG, 25, 7, 7, 2, 2, 1>, {}},
+  };
+  for (auto& a : arms) CK(hipFuncSetAttribute(a.kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  auto launch = [&](const void* k) {
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(k)), dim3(nsh * G), dim3(256), lds, st, A);
+  };
+  // parity: e1 vs e2 vs e2n1 after the chunk reduction
+  std::vector<std::vector<double>> res;
+  for (int k = 0; k < 3; ++k) {
+    launch(arms[k].kern);
+    CK(hipGetLastError());
+    CK(stk_launch_sweep_reduce(STK_LOGREG, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
+    std::vector<double> h((size_t)nsh * C * (Dp + 1));
+    CK(hipMemcpyAsync(h.data(), lp, sizeof(double) * nsh * C, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(h.data() + nsh * C, grad, sizeof(double) * nsh * C * Dp, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    res.push_back(h);
+  }
+  for (int k = 1; k < 3; ++k) {
+    double lpr = 0, gr = 0, gmax = 0;
+    for (int i = 0; i < nsh * C; ++i) lpr = std::max(lpr, fabs(res[k][i] - res[0][i]) / fabs(res[0][i]));
+    for (size_t i = nsh * C; i < res[0].size(); ++i) gmax = std::max(gmax, fabs(res[0][i]));
+    for (size_t i = nsh * C; i < res[0].size(); ++i) gr = std::max(gr, fabs(res[k][i] - res[0][i]) / gmax);
+    printf("parity %s vs e2er: lp max rel %.3g, grad max |diff| / max|grad| %.3g (lp[0] %.6f)\n", arms[k].name, lpr, gr,
+           res[0][0]);
+  }
+  for (int r = 0; r < rounds; ++r) {
+    for (auto& a : arms) {
+      launch(a.kern);
+      CK(hipStreamSynchronize(st));
+      CK(hipEventRecord(e0, st));
+      for (int i = 0; i < reps; ++i) launch(a.kern);
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      a.ms.push_back(ms / reps);
+      printf("round %d %-8s %8.3f ms  %7.1f GB/s  %.3f of 8 TB/s\n", r, a.name, ms / reps, bytes / (ms / reps) / 1e6,
+             bytes / (ms / reps) / 1e6 / 8000.0);
+      fflush(stdout);
+    }
+  }
+  for (auto& a : arms) {
+    std::vector<float> v = a.ms;
+    std::sort(v.begin(), v.end());
+    printf("median %-8s %8.3f ms  %.3f of 8 TB/s\n", a.name, v[v.size() / 2], bytes / v[v.size() / 2] / 1e6 / 8000.0);
+  }
+  return 0;
+}
