@@ -1035,6 +1035,25 @@ int consensus_run(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P,
   STK_HIP_CHECK(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
   const size_t per = (size_t)P * S;
+  // A sample covariance of S draws has rank <= S - 1: with S <= p (p = the largest weight block)
+  // every shard's covariance is singular.  numpy's inv then returns rounding noise of order 1/eps
+  // (or raises when a pivot happens to round to exactly zero) and the reference's combine is
+  // meaningless; here it is a LinAlgError, independent of rounding.
+  int pmax = P;
+  if (row_block) {
+    std::vector<int32_t> rb(P), cnt(P, 0);
+    STK_HIP_CHECK(hipMemcpy(rb.data(), row_block, sizeof(int32_t) * P, hipMemcpyDefault));
+    for (int i = 0; i < P; ++i) {
+      ARG_CHECK(rb[i] >= 0 && rb[i] < P, "row_block[%d] = %d out of [0, P)", i, rb[i]);
+      ++cnt[rb[i]];
+    }
+    pmax = *std::max_element(cnt.begin(), cnt.end());
+  }
+  if (S <= pmax) {
+    stk_set_error("%d draws give a singular sample covariance for a %d-parameter weight block (rank <= S - 1; "
+                  "LinAlgError)", S, pmax);
+    return STK_E_LINALG;
+  }
   CombineBufs b;
   RC(combine_bufs(ctx, nshards, P, S, &b));
   STK_HIP_CHECK(hipMemcpyAsync(b.X, draws, sizeof(double) * per * nshards, hipMemcpyDefault, st));

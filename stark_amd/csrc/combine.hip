@@ -15,7 +15,7 @@
 //   k_spd_inverse    W_s = inv(cov_s): block Gauss-Jordan on 16 x 16 tiles held in registers,
 //                    fp64 MFMA updates (P <= 128), diagonal pivots -- a covariance is
 //                    symmetric positive (semi)definite, where diagonal pivoting is stable
-//                    (Cholesky's argument); a pivot <= 0 or NaN is reported as singular
+//                    (Cholesky's argument); a pivot <= 64 P eps or NaN is reported as singular
 //                    (LinAlgError).  One workgroup per shard, shards in parallel.  P > 128
 //                    falls back to k_gj_inverse (partial pivoting, global memory).
 //   k_sum_w          sum_s W_s in shard order (NaN shards hold W = 0)
@@ -263,9 +263,9 @@ __global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t*
 // k with cross-lane shuffles and does the folded rank-1 step a_ij -= c_i r_j (c_k = a_kk - 1,
 // r_k = 1 + 1/a_kk, r_j = a_kj / a_kk: Gauss-Jordan with no per-element cases; with pivots <= 1
 // the folded terms do not cancel).  Shard b with used[b] == 0 (NaN draws) gets W = 0 and no
-// status; status[b] = 1 when a pivot is <= 0 or NaN (singular covariance: numpy's inv raises
-// LinAlgError).
-__device__ __forceinline__ int inv16(double (&a)[4], int lr, int lg) {
+// status; status[b] = 1 when a pivot is <= 64 P eps or NaN (a singular covariance; numpy's inv
+// raises LinAlgError only on an exactly zero LU pivot and otherwise returns rounding noise).
+__device__ __forceinline__ int inv16(double (&a)[4], int lr, int lg, double pmin) {
   int sing = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -275,7 +275,7 @@ __device__ __forceinline__ int inv16(double (&a)[4], int lr, int lg) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) rk[s] = __shfl(a[s], k + 16 * lg);   // a[k][g + 4s]
     const double piv = __shfl(a[ks], k + 16 * kg);         // a[k][k], wave-uniform
-    if (!(piv > 0.0)) sing = 1;
+    if (!(piv > pmin)) sing = 1;
     double ip = __builtin_amdgcn_rcp(piv);
     ip = fma(ip, fma(-piv, ip, 1.0), ip);
     ip = fma(ip, fma(-piv, ip, 1.0), ip);
@@ -304,6 +304,9 @@ __global__ __launch_bounds__(512) void k_spd_inverse(const double* Min, double* 
     if (tid == 0) status[b] = 0;
     return;
   }
+  // pivots of the unit-diagonal matrix lie in (0, 1]; one at the rounding level of the
+  // elimination (<= 64 P eps) means a numerically singular covariance, reported as singular
+  const double pmin = 64.0 * P * 2.220446049250313e-16;
   int sing = 0;
   if (tid < 128) {
     const double dii = tid < P ? M[(size_t)tid * P + tid] : 1.0;
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(512) void k_spd_inverse(const double* Min, double* 
   };
   if (w == 0) {
     double d0[4] = {T[0][0], T[0][1], T[0][2], T[0][3]};   // T(0, 0), symmetric: read as A layout
-    const int sg = inv16(d0, lr, lg);
+    const int sg = inv16(d0, lr, lg, pmin);
     publish(&pub[0][0][0], d0, sg);
   }
   __syncthreads();
@@ -395,7 +398,7 @@ __global__ __launch_bounds__(512) void k_spd_inverse(const double* Min, double* 
 #pragma unroll
               for (int s = 0; s < 4; ++s) d[s] = T[I][s];
             }
-          const int sg = inv16(d, lr, lg);
+          const int sg = inv16(d, lr, lg, pmin);
 #pragma unroll
           for (int I = 0; I < NT; ++I) {
             if (I == kb) {

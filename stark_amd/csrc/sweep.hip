@@ -817,11 +817,12 @@ __device__ __forceinline__ void logit_resid(double eta, uint32_t ymask, const do
   constexpr double L_HI = 0.005415212348452769;          // ln2/128 rounded to 32 significant bits: n L_HI exact
   constexpr double L_LO = -3.2819649005320973e-13;       // ln2/128 - L_HI
   const double t = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, eta) ^ ((uint64_t)ymask << 32));
-  const double a = fabs(t);
-  // n = rint(-a 128/ln2) from the low word, clamped at -128 * 1010 (a ~ 700): past it e is a
-  // positive number below 1e-290 instead of exp(-a) (|lt|, |dv| error < 1e-290)
+  // a = min(|t|, 700): past it e = exp(-700) ~ 1e-304 stands in for exp(-a) (|lt|, |dv| error
+  // < 1e-304), and n = rint(-a 128/ln2) >= -129,300 stays exact in the low word of the fma trick
+  // and 2^{n div 128} a normal scale (a NaN t gives a = 700 here; the cutoff select below keeps NaN)
+  const double a = fmin(fabs(t), 700.0);
   const double sn = fma(-a, INV_L, MAGIC);
-  const int ni = max((int)(uint32_t)__builtin_bit_cast(uint64_t, sn), -128 * 1010);
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
   const double n = (double)ni;
   double r = fma(-n, L_HI, -a);
   r = fma(-n, L_LO, r);
@@ -1069,7 +1070,17 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
 // ER: early release -- the forward's A operands (25 values per lane) are read into registers with
 // everything else the sub-tile needs BEFORE the forward, so the slot is refilled while the
 // forward, the residual and the backward all run (ER = 0: after the forward, round 2).
-template <int FAM, int KF, int JT, int ABL = 0, int RV = 2, int NACC = SE_NACC, int ER = 1>
+// AUX: cache-policy bits of the X / y LDS-DMA loads (2 = nt: X is streamed once per sweep, 80 GB
+// against a 256 MB MALL).
+// PRIO (wave issue priority, s_setprio): 1 = raised over the residual (the dependent VALU / LDS
+// table chain goes first, the other wave's MFMAs fill its gaps), 2 = raised from the top of the
+// sub-tile until the next DMA is issued.
+// PF: L2 prefetch distance 2 -- with the DMA of sub-tile k+1 the wave also touches every 64-B
+// sector of sub-tile k+2 (and its y) by 4-byte LDS-DMA loads into a 256-B dummy LDS area, so the
+// sub-tile is on its way into L2 one sub-tile early and its own DMA, one iteration later, is
+// served from L2: HBM latency leaves the wave's critical path without another 12.8 KB slot.
+template <int FAM, int KF, int JT, int ABL = 0, int RV = 2, int NACC = SE_NACC, int ER = 1, int AUX = 0, int PRIO = 0,
+          int PF = 0>
 __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   constexpr int C = SM_C, NW = SM_W, JTV = JT - 1, KP = 4 * KF, KB = KP + SE_BPAD;
   const int shard = A.shard0 + blockIdx.x / A.G;
@@ -1096,6 +1107,7 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   double* const sptab = bimg + C * KB;
   // ER: the 4 remainder columns (16 rows x 4) of the wave's sub-tile, kept past the slot's release
   double* const xst = sptab + LG_TAB + w * 64;
+  double* const pfd = sptab + LG_TAB + NW * 64 + w * 32;     // PF: 256-B dummy per wave
   constexpr bool R2 = FAM == STK_LOGREG && RV == 2;
   if constexpr (R2) logit_tables_init(sptab);
   else if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
@@ -1118,12 +1130,24 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
     const int u = w + NW * k;
     const int xoff = u * SBX;
     for (int j = 0; j < nx - 1; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(slot + j * 1024), 16, lane * 16, xoff + j * 1024, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(slot + j * 1024), 16, lane * 16, xoff + j * 1024, 0, AUX);
     if (lane < last_lanes)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(slot + (nx - 1) * 1024), 16, lane * 16,
-                                               xoff + (nx - 1) * 1024, 0, 0);
+                                               xoff + (nx - 1) * 1024, 0, AUX);
     if (lane < SM_R * YB / 4)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_vptr)(slot + SBX), 4, lane * 4, u * SM_R * YB, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_vptr)(slot + SBX), 4, lane * 4, u * SM_R * YB, 0, AUX);
+  };
+  // PF touches: ceil(SBX / 4096) loads of one dword per 64-B sector + one for y -- a fixed count
+  // per sub-tile (every instruction has at least one active lane), so the DMA of sub-tile k is
+  // waited for with a counted vmcnt that leaves the touches of sub-tile k+1 in flight
+  const int npf = ((SBX + 4095) >> 12) + 1;
+  auto touch = [&](int k) {
+    const int u = w + NW * k;
+    const int xoff = u * SBX;
+    for (int j = 0; j < npf - 1; ++j)
+      if (j * 4096 + lane * 64 < SBX)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)pfd, 4, lane * 64, xoff + j * 4096, 0, 0);
+    if (lane == 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_vptr)pfd, 4, 0, u * SM_R * YB, 0, 0);
   };
 
   dbl4 gacc[JTV];
@@ -1135,9 +1159,12 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   const double* brow = bimg + lr * KB + lh * KF;
 
   if (mine > 0) issue(0);
+  if (PF && mine > 1) touch(1);
   for (int k = 0; k < mine; ++k) {
-    __builtin_amdgcn_s_waitcnt(0xF70);                   // vmcnt(0): sub-tile k landed
+    if (PF && k + 1 < mine) wait_vmcnt(npf);             // sub-tile k landed, the touches of k+1 may fly
+    else __builtin_amdgcn_s_waitcnt(0xF70);              // vmcnt(0): sub-tile k landed
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(2);
     const int rv = std::min(SM_R, nrows - SM_R * (w + NW * k));
     // ---- forward (ER: operands first, MFMAs after the slot is released)
     dbl4 ea[NACC];
@@ -1180,6 +1207,8 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
     __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): the slot is free
     __builtin_amdgcn_sched_barrier(0);
     if (k + 1 < mine) issue(k + 1);
+    if (PF && k + 2 < mine) touch(k + 2);
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (ER && !(ABL & 4)) {
 #pragma unroll
@@ -1193,6 +1222,10 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
 
     // ---- residual
     double de[4];
+    if constexpr (PRIO == 1) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(2);
+    }
     if constexpr (R2 && !(ABL & 1)) {
       if (rv == SM_R) {                                  // full sub-tile (all but a chunk's last): no masks
 #pragma unroll
@@ -1240,6 +1273,10 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
       lpa += valid ? lt : 0.0;
       gaa += dv;
       de[i] = dv;
+    }
+    if constexpr (PRIO == 1) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
     }
     // ---- backward
     if constexpr (!(ABL & 2)) {
@@ -1769,7 +1806,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *G = (int)g;
     const int JT = (d + 15) / 16;
     size_t ring = (size_t)SM_W * nb * sweepm_slot_bytes(d) + LG_TAB * sizeof(double);
-    if (d == 100) ring = (size_t)SM_W * sweepm_slot_bytes(d) + (16 * (100 + SE_BPAD) + std::max(SP_TAB, LG_TAB) + SM_W * 64) * sizeof(double);   // v4e
+    if (d == 100) ring = (size_t)SM_W * sweepm_slot_bytes(d) + (16 * (100 + SE_BPAD) + std::max(SP_TAB, LG_TAB) + SM_W * 64 + SM_W * 32) * sizeof(double);   // v4e
     const size_t red = ((size_t)SM_W * JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * sizeof(double);
     *lds_bytes = std::max(ring, red);
     return;

@@ -68,6 +68,29 @@ def test_regression_lpgrad(ctx, orc, family, n, d, C):
         assert np.all(np.abs(g[c] - og) <= RTOL_LP * np.maximum(np.abs(og), scale * 1e-3)), (c, np.abs(g[c] - og).max())
 
 
+@pytest.mark.parametrize("scale", [30.0, 1e3, 1e8, 1e150])
+@pytest.mark.parametrize("n,d,C", [(2000, 100, 16), (999, 50, 16), (300, 40, 16), (500, 100, 64), (400, 60, 4)])
+def test_logistic_lpgrad_extreme_eta(ctx, orc, scale, n, d, C):
+    """|eta| from ~1 to ~1e151 (NUTS step-size probes from a dispersed init reach such points):
+    Stan's +-20 cutoffs -- lt = t, dv = +-1 below, lt ~ -exp(-t) ~ 0 above -- through the
+    table-driven residual of k_sweepe / k_sweepm / pass F (|t| is clamped at 700 before the
+    exp) and the VALU sweeps, vs the oracle."""
+    from stark_amd import engine
+    rng = np.random.default_rng(int(scale) % 1000 + n)
+    X = rng.uniform(-1.7, 1.7, (n, d))
+    y = (rng.uniform(size=n) < 0.5).astype(np.int32)
+    om = orc.Model(orc.FAM_LOGREG, X=X, y=y)
+    m = engine.Model(ctx, "logistic", [{"x": X, "y": y}])
+    q = rng.normal(0, 1.0 / np.sqrt(d), (C, om.D))
+    q[: C // 2] *= scale
+    lp, g = m.log_density_grad(0, q)
+    for c in range(C):
+        olp, og = om.lpgrad(q[c])
+        assert np.isfinite(lp[c]) and _rel(lp[c], olp) < RTOL_LP, (c, lp[c], olp)
+        gs = np.abs(og).max() + 1.0
+        assert np.all(np.abs(g[c] - og) <= RTOL_LP * np.maximum(np.abs(og), gs * 1e-3)), (c, np.abs(g[c] - og).max())
+
+
 # ---------------------------------------------------------------- synthetic generator
 @pytest.mark.parametrize("d", [1, 7, 100])
 def test_synthetic_generator_matches_oracle(ctx, orc, d):
@@ -147,9 +170,10 @@ def test_combine_public_solve_is_a_general_inverse(ctx):
 def test_combine_rank_deficient_covariance(ctx, golden, P):
     """S - 1 < P draws: each sample covariance is singular.  The reference's np.linalg.inv does
     not raise on it (LAPACK LU meets no exactly zero pivot) and returns an 'inverse' made of
-    rounding noise (tests/golden/make_golden.py records it); the GPU combine, which inverts
-    covariances by diagonal pivoting, reports the singular covariance as LinAlgError -- the
-    documented deviation (include/stark_hip.h)."""
+    rounding noise (tests/golden/make_golden.py records it); the GPU combine reports it as
+    LinAlgError, decided by the rank bound S - 1 < p before any arithmetic (not by the sign of a
+    rounded pivot) -- the documented deviation (include/stark_hip.h).  Also
+    through the blocked call (p = the larger weight block) and the pairwise reducer."""
     from stark_amd import engine
     from stark_amd._lib import LinAlgError
     g = golden("combine_ref.npz")
@@ -157,6 +181,17 @@ def test_combine_rank_deficient_covariance(ctx, golden, P):
     assert f1.shape[1] - 1 < P and int(g[f"rankdef_P{P}_raised"]) == 0
     with pytest.raises(LinAlgError):
         engine.consensus([f1, f2], ctx)
+    with pytest.raises(LinAlgError):
+        engine.consensus([f1, f2], ctx, separate_lp=True)
+    with pytest.raises(LinAlgError):
+        engine.consensus_products([f1, f2], ctx)
+    # one draw more than the largest block: full rank, combined
+    rng = np.random.default_rng(P)
+    ok = [rng.normal(size=(P, P + 1)) for _ in range(2)]
+    out, used = engine.consensus(ok, ctx)
+    assert used.all() and np.isfinite(out).all()
+    blk, _ = engine.consensus([x[:, :P] for x in ok], ctx, separate_lp=True)   # blocks P - 1 and 1, S = P
+    assert np.isfinite(blk).all()
 
 
 def test_combine_device_draws_match_host(ctx):

@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 3, call f: k_sweepe A/B (nt DMA, L2 prefetch touches, wave priority) at the bench
+# geometry; PMC of every arm (clock, MFMA busy, waits); which VALU classes share the fp64 pipe
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r03f
+mkdir -p $O
+timeout -k 10 300 tools/_bin/sweepe_ab 12500000 8 3 8 > $O/sweepe_ab.log 2>&1
+rc=$?; echo "sweepe_ab rc=$rc"; grep -E "parity|median" $O/sweepe_ab.log; [ $rc -eq 0 ] || exit 3
+timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d $O/pmc1 -o pmc --output-format csv -- tools/_bin/sweepe_ab 12500000 8 1 1 > $O/pmc1.log 2>&1
+rc=$?; echo "pmc1 rc=$rc"; [ $rc -eq 0 ] || exit 4
+timeout -k 10 150 tools/_bin/valu_mix > $O/valu_mix.log 2>&1
+rc=$?; echo "valu_mix rc=$rc"; cat $O/valu_mix.log

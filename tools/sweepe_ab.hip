@@ -83,18 +83,23 @@ int main(int argc, char** argv) {
   std::vector<Arm> arms = {
       {"e2er", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 1>, {}},
       {"e2", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 0>, {}},
-      {"e1", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 1, 2, 0>, {}},
-      {"e2er-fwd", (const void*)k_sweepe<STK_LOGREG, 25, 7, 4, 2, 2, 1>, {}},
-      {"e2er-bwd", (const void*)k_sweepe<STK_LOGREG, 25, 7, 2, 2, 2, 1>, {}},
-      {"e2er-all", (const void*)k_sweepe<STK_LOGREG, 25, 7, 7, 2, 2, 1>, {}},
+      {"e2-nt", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 0, 2>, {}},
+      {"e2-nt-p1", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 0, 2, 1>, {}},
+      {"e2er-pf", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 1, 0, 0, 1>, {}},
+      {"e2-pf", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 0, 0, 0, 1>, {}},
+      {"e2er-nt-pf", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 1, 2, 0, 1>, {}},
+      {"e2-nt-pf", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 0, 2, 0, 1>, {}},
+      {"e2er-nt-pf-p1", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 1, 2, 1, 1>, {}},
+      {"e2-all-nt", (const void*)k_sweepe<STK_LOGREG, 25, 7, 7, 2, 2, 0, 2>, {}},
+      {"e2-all-nt-pf", (const void*)k_sweepe<STK_LOGREG, 25, 7, 7, 2, 2, 0, 2, 0, 1>, {}},
   };
   for (auto& a : arms) CK(hipFuncSetAttribute(a.kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   auto launch = [&](const void* k) {
     hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(k)), dim3(nsh * G), dim3(256), lds, st, A);
   };
-  // parity: e1 vs e2 vs e2n1 after the chunk reduction
+  // parity: every arm with arithmetic vs e2er after the chunk reduction
   std::vector<std::vector<double>> res;
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < 9; ++k) {
     launch(arms[k].kern);
     CK(hipGetLastError());
     CK(stk_launch_sweep_reduce(STK_LOGREG, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
@@ -104,7 +109,7 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(st));
     res.push_back(h);
   }
-  for (int k = 1; k < 3; ++k) {
+  for (int k = 1; k < 9; ++k) {
     double lpr = 0, gr = 0, gmax = 0;
     for (int i = 0; i < nsh * C; ++i) lpr = std::max(lpr, fabs(res[k][i] - res[0][i]) / fabs(res[0][i]));
     for (size_t i = nsh * C; i < res[0].size(); ++i) gmax = std::max(gmax, fabs(res[0][i]));
