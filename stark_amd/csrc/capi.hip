@@ -297,6 +297,22 @@ int stk_model_create(stk_ctx* ctx, int family, const stk_shard* shards, int nsha
       sd.x = (const double*)p;
       if (family == STK_LOGREG) {
         if (!in.y_int) { stk_set_error("shard %d: logreg needs y_int", s); rc = STK_E_ARG; break; }
+        {   // bernoulli_logit: y in {0, 1} (the sweeps read y as a sign bit)
+          std::vector<int32_t> yh(in.n_rows);
+          if (hipMemcpy(yh.data(), in.y_int, sizeof(int32_t) * in.n_rows, hipMemcpyDefault) != hipSuccess) {
+            stk_set_error("shard %d: y_int is not readable", s);
+            rc = STK_E_ARG;
+            break;
+          }
+          int64_t bad = -1;
+          for (int64_t i = 0; i < in.n_rows && bad < 0; ++i)
+            if (yh[i] != 0 && yh[i] != 1) bad = i;
+          if (bad >= 0) {
+            stk_set_error("shard %d: y_int[%lld] = %d; bernoulli_logit needs 0 or 1", s, (long long)bad, yh[bad]);
+            rc = STK_E_ARG;
+            break;
+          }
+        }
         if ((rc = upload(m, in.y_int, sizeof(int32_t) * in.n_rows, &p))) break;
         sd.yi = (const int32_t*)p;
       } else {

@@ -848,6 +848,65 @@ __device__ __forceinline__ void logit_resid(double eta, uint32_t ymask, const do
   dv = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, dvp) ^ ((uint64_t)ymask << 32));
 }
 
+// Logistic residual v3 (k_sweepe RV = 3): v2 with fewer VALU instructions -- on gfx950 EVERY
+// vector instruction (f64, f32, int, select) takes the issue slot the f64 MFMA needs
+// (tools/valu_mix.hip: no class overlaps v_mfma_f64_16x16x4), so the residual's instruction
+// count, not its f64 count, is what it costs.  Same quantities and cutoffs as v2:
+//   Stan's lower cutoff without selects: a = min(|t| + 2^60 max(-20 - t, 0), 700) is |t| for
+//   t >= -20 and 700 below, where e = exp(-700) ~ 1e-304 makes lg = e, lt = t - lg = t and
+//   dv/sgn = 1/(1 + e) = 1 exactly -- Stan's (t, 1);
+//   exp(-a): 256-entry 2^{j/256} table, |r| <= ln2/512, degree-4 Taylor (rel. error 4e-17), the
+//   2^{n div 256} scale by v_ldexp_f64;  log1p(e): 257-entry [c_j, d_j, l_j] table (j = rint(256 e)),
+//   |rl| <= 1/512, degree-4 fitted q (abs. error 1.2e-18);
+//   lt = t/2 - (|t|/2 + lg) = min(t, 0) - lg with NaN kept (a NaN eta gives a NaN lp; t = +inf
+//   gives NaN where Stan's upper branch gives 0 -- a point no finite beta reaches).
+// About 38 vector instructions per (row, chain) against v2's ~50.
+constexpr int LG3_TAB = 256 + 4 * 257;     // doubles: T[256], then [c_j, d_j, l_j, 0] for j = 0..256
+__device__ void logit3_tables_init(double* tab) {
+  for (int i = threadIdx.x; i < LG3_TAB; i += blockDim.x) {
+    double v;
+    if (i < 256) {
+      v = exp2((double)i / 256.0);
+    } else {
+      const int j = (i - 256) >> 2, f = (i - 256) & 3;
+      v = f == 0 ? 256.0 / (256 + j) : (f == 1 ? (double)j / (256 + j) : (f == 2 ? log1p((double)j / 256.0) : 0.0));
+    }
+    tab[i] = v;
+  }
+}
+
+__device__ __forceinline__ void logit_resid3(double eta, uint32_t ymask, const double* tab, double& lt, double& dv) {
+  constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
+  constexpr double INV_L = 369.3299304675746;             // 256 / ln 2
+  constexpr double L_HI = 0.0027076061742263846;          // ln2/256 to 32 significant bits: n L_HI exact
+  constexpr double L_LO = -1.6409824498184568e-13;        // ln2/256 - L_HI
+  constexpr double Q1 = -0.4999999999996968, Q2 = 0.33333333333269194, Q3 = -0.25000063579045223,
+                   Q4 = 0.2000006787837857;               // log(1+x)/x on |x| <= 1/512 (tools: least squares)
+  const double t = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, eta) ^ ((uint64_t)ymask << 32));
+  const double a = fmin(fma(fmax(-20.0 - t, 0.0), 1152921504606846976.0, fabs(t)), 700.0);   // + 2^60 max(-20 - t, 0)
+  const double sn = fma(-a, INV_L, MAGIC);
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
+  const double n = sn - MAGIC;
+  double r = fma(-n, L_HI, -a);
+  r = fma(-n, L_LO, r);
+  const double p = fma(fma(fma(fma(1.0 / 24.0, r, 1.0 / 6.0), r, 0.5), r, 1.0), r, 1.0);
+  const double e = __builtin_amdgcn_ldexp(tab[ni & 255] * p, ni >> 8);
+  const int j = (int)fma(e, 256.0, 0.5);                  // rint(256 e), e in [0, 1] (v_cvt_i32_f64 truncates)
+  const double* cj = tab + 256 + 4 * j;
+  const dbl2 cd = *reinterpret_cast<const dbl2*>(cj);
+  const double rl = fma(e, cd.x, -cd.y);
+  const double q = fma(fma(fma(fma(Q4, rl, Q3), rl, Q2), rl, Q1), rl, 1.0);
+  const double lg = fma(rl, q, cj[2]);
+  const double u = 1.0 + e;
+  double ri = __builtin_amdgcn_rcp(u);
+  ri = fma(ri, fma(-u, ri, 1.0), ri);
+  const double w = e * ri;
+  const uint32_t neg = (uint32_t)((int32_t)(__builtin_bit_cast(uint64_t, t) >> 32) >> 31);   // ~0u when t < 0
+  const double dvp = blend(neg, ri, w);
+  dv = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, dvp) ^ ((uint64_t)ymask << 32));
+  lt = fma(0.5, t, fma(-0.5, fabs(t), -lg));
+}
+
 // ABL (micro-benchmark ablations only): bit 0 linear residual stand-in, bit 1 no backward,
 // bit 2 no forward.  KFS/JTS: compile-time KF / JT for the BASELINE shapes (0 = runtime).
 template <int FAM, int KFS = 0, int JTS = 0, int ABL = 0, int MINB = SM_MINB, bool VREM = false>
@@ -1079,8 +1138,14 @@ __global__ __launch_bounds__(256, MINB) void k_sweepm(SweepArgs A, int NB) {
 // sector of sub-tile k+2 (and its y) by 4-byte LDS-DMA loads into a 256-B dummy LDS area, so the
 // sub-tile is on its way into L2 one sub-tile early and its own DMA, one iteration later, is
 // served from L2: HBM latency leaves the wave's critical path without another 12.8 KB slot.
+// IL: on full sub-tiles the residual and the backward run in two halves (rows 0-1, then 2-3 of the
+// lane's four): half the residual's live registers, and the first half's backward MFMAs are
+// independent of the second half's residual chain (same summation order: bitwise the same result).
+// FS (ER = 0): the forward's operand reads and the reads of everything else the sub-tile needs
+// from the slot are interleaved with the forward MFMAs two ds_reads per MFMA (sched_group_barrier),
+// so the LDS latency hides behind MFMAs and the slot is free when the last forward MFMA issues.
 template <int FAM, int KF, int JT, int ABL = 0, int RV = 2, int NACC = SE_NACC, int ER = 1, int AUX = 0, int PRIO = 0,
-          int PF = 0>
+          int PF = 0, int IL = 0, int FS = 0>
 __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   constexpr int C = SM_C, NW = SM_W, JTV = JT - 1, KP = 4 * KF, KB = KP + SE_BPAD;
   const int shard = A.shard0 + blockIdx.x / A.G;
@@ -1106,10 +1171,12 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   double* const bimg = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);  // [16][KB]
   double* const sptab = bimg + C * KB;
   // ER: the 4 remainder columns (16 rows x 4) of the wave's sub-tile, kept past the slot's release
-  double* const xst = sptab + LG_TAB + w * 64;
-  double* const pfd = sptab + LG_TAB + NW * 64 + w * 32;     // PF: 256-B dummy per wave
-  constexpr bool R2 = FAM == STK_LOGREG && RV == 2;
-  if constexpr (R2) logit_tables_init(sptab);
+  constexpr int TABN = RV == 3 ? LG3_TAB : LG_TAB;
+  double* const xst = sptab + TABN + w * 64;
+  double* const pfd = sptab + TABN + NW * 64 + w * 32;       // PF: 256-B dummy per wave
+  constexpr bool R2 = FAM == STK_LOGREG && RV >= 2;
+  if constexpr (FAM == STK_LOGREG && RV == 3) logit3_tables_init(sptab);
+  else if constexpr (R2) logit_tables_init(sptab);
   else if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
   const double* qs = A.q + (size_t)shard * C * A.Dp;
   for (int i = tid; i < C * KP; i += NW * 64) {
@@ -1198,10 +1265,19 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
         xv[i][1] = p[1];
       }
       if constexpr (R2) {
-        ym[i] = (uint32_t)(*reinterpret_cast<const int32_t*>(slot + SBX + (lh + 4 * i) * 4) == 0) << 31;
+        // y in {0, 1}: (y << 31) + 2^31 = 2^31 for y = 0, 0 for y = 1 (one v_lshl_add_u32)
+        ym[i] = ((uint32_t)*reinterpret_cast<const int32_t*>(slot + SBX + (lh + 4 * i) * 4) << 31) + 0x80000000u;
       } else {
         yv[i] = (FAM == STK_LOGREG) ? (double)*reinterpret_cast<const int32_t*>(slot + SBX + (lh + 4 * i) * 4)
                                     : *reinterpret_cast<const double*>(slot + SBX + (lh + 4 * i) * 8);
+      }
+    }
+    if constexpr (FS && !ER && !(ABL & 4)) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);         // 6 ds_reads ahead
+#pragma unroll
+      for (int s = 0; s < KF; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // 2 ds_reads
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): the slot is free
@@ -1226,21 +1302,48 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(2);
     }
+    bool bwd_done = false;
+    auto bwd_rows = [&](int s0, int s1) {              // backward MFMAs + remainder columns of rows s0..s1-1
+#pragma unroll
+      for (int s = s0; s < s1; ++s)
+#pragma unroll
+        for (int t = 0; t < JTV; ++t) gacc[t] = mfma_f64(xa[s][t], de[s], gacc[t]);
+#pragma unroll
+      for (int i = s0; i < s1; ++i) {
+        if constexpr (ER) {
+          const dbl2* p = reinterpret_cast<const dbl2*>(xst + (lh + 4 * i) * 4);
+          xv[i][0] = p[0];
+          xv[i][1] = p[1];
+        }
+        gv[0] = fma(xv[i][0].x, de[i], gv[0]);
+        gv[1] = fma(xv[i][0].y, de[i], gv[1]);
+        gv[2] = fma(xv[i][1].x, de[i], gv[2]);
+        gv[3] = fma(xv[i][1].y, de[i], gv[3]);
+      }
+    };
     if constexpr (R2 && !(ABL & 1)) {
       if (rv == SM_R) {                                  // full sub-tile (all but a chunk's last): no masks
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          double lt;
-          logit_resid(eta4[i], ym[i], sptab, lt, de[i]);
-          lpa += lt;
-          gaa += de[i];
+        for (int h = 0; h < (IL ? 2 : 1); ++h) {
+          const int i0 = IL ? 2 * h : 0, i1 = IL ? 2 * h + 2 : 4;
+#pragma unroll
+          for (int i = i0; i < i1; ++i) {
+            double lt;
+            if constexpr (RV == 3) logit_resid3(eta4[i], ym[i], sptab, lt, de[i]);
+            else logit_resid(eta4[i], ym[i], sptab, lt, de[i]);
+            lpa += lt;
+            gaa += de[i];
+          }
+          if constexpr (IL && !(ABL & 2)) bwd_rows(i0, i1);
         }
+        bwd_done = IL;
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const bool valid = lh + 4 * i < rv;
           double lt, dv;
-          logit_resid(eta4[i], ym[i], sptab, lt, dv);
+          if constexpr (RV == 3) logit_resid3(eta4[i], ym[i], sptab, lt, dv);
+          else logit_resid(eta4[i], ym[i], sptab, lt, dv);
           dv = valid ? dv : 0.0;
           lpa += valid ? lt : 0.0;
           gaa += dv;
@@ -1280,22 +1383,7 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
     }
     // ---- backward
     if constexpr (!(ABL & 2)) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int t = 0; t < JTV; ++t) gacc[t] = mfma_f64(xa[s][t], de[s], gacc[t]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (ER) {
-          const dbl2* p = reinterpret_cast<const dbl2*>(xst + (lh + 4 * i) * 4);
-          xv[i][0] = p[0];
-          xv[i][1] = p[1];
-        }
-        gv[0] = fma(xv[i][0].x, de[i], gv[0]);
-        gv[1] = fma(xv[i][0].y, de[i], gv[1]);
-        gv[2] = fma(xv[i][1].x, de[i], gv[2]);
-        gv[3] = fma(xv[i][1].y, de[i], gv[3]);
-      }
+      if (!bwd_done) bwd_rows(0, 4);
     }
   }
 
@@ -1806,7 +1894,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *G = (int)g;
     const int JT = (d + 15) / 16;
     size_t ring = (size_t)SM_W * nb * sweepm_slot_bytes(d) + LG_TAB * sizeof(double);
-    if (d == 100) ring = (size_t)SM_W * sweepm_slot_bytes(d) + (16 * (100 + SE_BPAD) + std::max(SP_TAB, LG_TAB) + SM_W * 64 + SM_W * 32) * sizeof(double);   // v4e
+    if (d == 100) ring = (size_t)SM_W * sweepm_slot_bytes(d) + (16 * (100 + SE_BPAD) + std::max(SP_TAB, std::max(LG_TAB, LG3_TAB)) + SM_W * 64 + SM_W * 32) * sizeof(double);   // v4e
     const size_t red = ((size_t)SM_W * JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * sizeof(double);
     *lds_bytes = std::max(ring, red);
     return;
@@ -1906,7 +1994,9 @@ static hipError_t launch_sweepm(const SweepArgs& A, int d, int nblocks, size_t l
     return hipGetLastError();
   };
   if (d == 100) {
-    auto kern = k_sweepe<FAM, 25, 7>;
+    // residual v3, slot released after the forward (ER = 0), nt DMA, residual at raised priority
+    // (tools/sweepe_ab.hip A/B: 15.44 -> 14.59 ms against the round-2 configuration on one box)
+    auto kern = k_sweepe<FAM, 25, 7, 0, 3, SE_NACC, 0, 2, 1>;
     if (const hipError_t e = allow_big_lds((const void*)kern)) return e;
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A);
     return hipGetLastError();
