@@ -200,13 +200,16 @@ STK_API int stk_transition(stk_model* m, int shard, double* q, int32_t C, uint64
                            double eps, const double* inv_metric, int32_t max_depth, double* lp, double* stats);
 
 /* ---- consensus combine: stark/stark.py:7-21, 66-70 ---- */
-/* draws: nshards x P x S (host or device memory).  shard_used[s] = 0 for shards left out
- * because of NaN draws.  Singular matrices (STK_E_LINALG, numpy's LinAlgError):
+/* draws: nshards x P x S, out: P x S (host or device memory; device buffers are read and
+ * written in place, host buffers staged through the context).  shard_used[s] = 0 for shards
+ * left out because of NaN draws.  Singular matrices (STK_E_LINALG, numpy's LinAlgError):
  *   - stk_consensus / _blocked / _products invert each sample covariance and sum W, which are
- *     symmetric positive (semi)definite by construction, by diagonal-pivot block Gauss-Jordan and
- *     report a pivot <= 0 or NaN as singular.  A rank-deficient covariance (S - 1 < P, collinear
- *     rows) therefore raises here, where np.linalg.inv's LU usually returns a huge finite
- *     "inverse" built from rounding noise;
+ *     symmetric positive (semi)definite by construction, by diagonal-pivot block Gauss-Jordan on
+ *     the unit-diagonal matrix and report a pivot <= 64 P eps or NaN as singular.  S <= p draws
+ *     (p = P, or the largest row_block block) give a rank-deficient covariance (rank <= S - 1)
+ *     and raise before any arithmetic; np.linalg.inv's LU usually returns a huge finite
+ *     "inverse" built from rounding noise there, and raises only on an exactly zero pivot (a
+ *     constant row: both raise) -- DESIGN.md section 9;
  *   - stk_consensus_solve takes the caller's sum W as ANY square matrix (symmetric or not) and
  *     inverts it as np.linalg.inv does, by partial pivoting, singular only on an exactly zero
  *     pivot. */

@@ -1044,6 +1044,16 @@ int combine_check(const std::vector<int32_t>& h, int nshards, int32_t* shard_use
   }
   return STK_OK;
 }
+// device memory (hipMalloc / a torch cuda tensor): the combine reads the draws and writes the
+// result in place instead of staging them through the context's scratch buffers
+bool is_device_ptr(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice;
+}
 int consensus_run(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S, const int32_t* row_block,
                   double* sum_w, double* sum_wtheta, double* out, int32_t* shard_used) {
   ARG_CHECK(ctx && draws && nshards > 0 && P > 0 && S > 1, "stk_consensus: bad arguments");
@@ -1072,12 +1082,15 @@ int consensus_run(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P,
   }
   CombineBufs b;
   RC(combine_bufs(ctx, nshards, P, S, &b));
-  STK_HIP_CHECK(hipMemcpyAsync(b.X, draws, sizeof(double) * per * nshards, hipMemcpyDefault, st));
+  const bool dev_in = is_device_ptr(draws), dev_out = out && is_device_ptr(out);
+  const double* X = dev_in ? draws : b.X;
+  if (!dev_in) STK_HIP_CHECK(hipMemcpyAsync(b.X, draws, sizeof(double) * per * nshards, hipMemcpyDefault, st));
   if (row_block) STK_HIP_CHECK(hipMemcpyAsync(b.blk, row_block, sizeof(int32_t) * P, hipMemcpyDefault, st));
-  STK_HIP_CHECK(stk_launch_consensus_products(b.X, nshards, P, S, row_block ? b.blk : nullptr, b.mean, b.rowbad,
+  STK_HIP_CHECK(stk_launch_consensus_products(X, nshards, P, S, row_block ? b.blk : nullptr, b.mean, b.rowbad,
                                               b.used, b.status, b.cov, b.W, b.work, b.sw, b.swt, st));
   if (out)
-    STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status + nshards, b.out, st, false));
+    STK_HIP_CHECK(stk_launch_consensus_solve(b.sw, b.swt, P, S, b.inv, b.work, b.status + nshards,
+                                             dev_out ? out : b.out, st, false));
   std::vector<int32_t> h(2 * nshards + 1, 0);
   STK_HIP_CHECK(hipMemcpyAsync(h.data(), b.used, sizeof(int32_t) * (2 * nshards + (out ? 1 : 0)), hipMemcpyDeviceToHost, st));
   STK_HIP_CHECK(hipStreamSynchronize(st));
@@ -1088,8 +1101,8 @@ int consensus_run(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P,
   }
   if (sum_w) STK_HIP_CHECK(hipMemcpyAsync(sum_w, b.sw, sizeof(double) * P * P, hipMemcpyDefault, st));
   if (sum_wtheta) STK_HIP_CHECK(hipMemcpyAsync(sum_wtheta, b.swt, sizeof(double) * per, hipMemcpyDefault, st));
-  if (out) STK_HIP_CHECK(hipMemcpyAsync(out, b.out, sizeof(double) * per, hipMemcpyDefault, st));
-  STK_HIP_CHECK(hipStreamSynchronize(st));
+  if (out && !dev_out) STK_HIP_CHECK(hipMemcpyAsync(out, b.out, sizeof(double) * per, hipMemcpyDefault, st));
+  if (sum_w || sum_wtheta || (out && !dev_out)) STK_HIP_CHECK(hipStreamSynchronize(st));
   return STK_OK;
 }
 }  // namespace
