@@ -92,8 +92,22 @@ __device__ __forceinline__ double log_sum_exp2(double a, double b) {   // stan::
 // ------------------------------------------------------------------ model hooks
 // 8 schools (example/schools.stan:1-18): q = (mu, log tau, eta_1..J); returns lp, writes
 // grad lp.  Mirrors oracle orc_schools_lpgrad.
+// y_j and sigma_j of this lane's schools (element e = k SEG + lane is school e - 2), loaded once
+// per launch instead of two global loads per leapfrog (their latency was on every leapfrog's
+// critical path at one wave per SIMD)
 template <int NCH, int SEG = WAVE>
-__device__ double schools_lpgrad(const ShardDev& sh, const double (&q)[NCH], double (&glp)[NCH], int lane, int D) {
+__device__ __forceinline__ void schools_data(const ShardDev& sh, double (&yc)[NCH], double (&sc)[NCH], int lane, int D) {
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int e = k * SEG + lane;
+    const bool in = e >= 2 && e < D;
+    yc[k] = in ? sh.y[e - 2] : 0.0;
+    sc[k] = in ? sh.sigma[e - 2] : 1.0;
+  }
+}
+template <int NCH, int SEG = WAVE>
+__device__ double schools_lpgrad(const double (&yc)[NCH], const double (&sc)[NCH], const double (&q)[NCH],
+                                 double (&glp)[NCH], int lane, int D) {
   const double mu = seg_bcast<SEG>(q[0], 0);
   const double u = seg_bcast<SEG>(q[0], 1);
   const double tau = exp(u);
@@ -103,11 +117,10 @@ __device__ double schools_lpgrad(const ShardDev& sh, const double (&q)[NCH], dou
     const int e = k * SEG + lane;
     glp[k] = 0.0;
     if (e >= 2 && e < D) {
-      const int j = e - 2;
       const double eta = q[k];
       const double theta = mu + tau * eta;
-      const double sj = sh.sigma[j];
-      const double z = (sh.y[j] - theta) / sj;
+      const double sj = sc[k];
+      const double z = (yc[k] - theta) / sj;
       const double r = z / sj;
       lp += -0.5 * eta * eta - 0.5 * z * z;
       smu += r;
@@ -167,18 +180,21 @@ struct NutsChain {
   double s[S_COUNT];
   int iv[I_COUNT];
   double q[NCH], p[NCH], g[NCH], im[NCH];
+  uint32_t nleap = 0, ndiv = 0;   // leapfrogs / divergent draws since the last flush_counts()
 
   __device__ __forceinline__ NutsChain(const NutsArgs& a, int gid_, int lane_)
       : NutsChain(a, gid_, lane_, a.vec + (size_t)gid_ * V_COUNT * a.Dp,
                   a.stk + (size_t)gid_ * a.max_depth * SV_COUNT * a.Dp) {}
-  // vec_ / stk_: this chain's vector block and tree stack (global memory, or an LDS copy)
-  __device__ __forceinline__ NutsChain(const NutsArgs& a, int gid_, int lane_, double* vec_, double* stk_)
+  // vec_ / stk_ / stks_: this chain's vector block, tree stack and stack scalars (global memory,
+  // or LDS copies)
+  __device__ __forceinline__ NutsChain(const NutsArgs& a, int gid_, int lane_, double* vec_, double* stk_,
+                                       double* stks_ = nullptr)
       : A(a), gid(gid_), lane(lane_), shard(gid_ / a.C), cidx(gid_ % a.C), D(a.shards[gid_ / a.C].D),
         rid(rng_stream(a, gid_)),
         sh(a.shards[gid_ / a.C]),
         vec(vec_),
         stk(stk_),
-        stks(a.stks + (size_t)gid_ * a.max_depth * SS_COUNT) {}
+        stks(stks_ ? stks_ : a.stks + (size_t)gid_ * a.max_depth * SS_COUNT) {}
 
   __device__ __forceinline__ bool ok(int k) const { return k * SEG + lane < D; }
   __device__ __forceinline__ double* vp(int v) const { return vec + (size_t)v * A.Dp; }
@@ -213,6 +229,13 @@ struct NutsChain {
     ld(vp(V_G), g);
     ld(vp(V_IM), im);
   }
+  __device__ __forceinline__ void flush_counts() {
+    if (lane == 0 && (nleap | ndiv)) {
+      A.cnt[(size_t)gid * C_COUNT + C_LEAP] += nleap;
+      A.cnt[(size_t)gid * C_COUNT + C_DIV] += ndiv;
+    }
+    nleap = ndiv = 0;
+  }
   __device__ __forceinline__ void save() const {
     double* sc = A.sc + (size_t)gid * S_COUNT;
     int* ivp = A.iv + (size_t)gid * I_COUNT;
@@ -241,9 +264,18 @@ struct NutsChain {
     b = seg_sum<SEG>(b);
     return a > 0 && b > 0;
   }
+  // uniforms k = 2m and 2m + 1 of a transition come from one Philox block: the odd one is kept
+  // from the even one's call (u_key = the block's (iteration, m) + 1; 0 = nothing kept)
+  uint64_t u_odd = 0, u_key = 0;
   __device__ __forceinline__ double uniform() {
     const uint32_t it = (uint32_t)(iv[I_ITER] + A.iter_offset);
-    return uniform_at(A.seed, rid, it, (uint32_t)iv[I_UK]++, TAG_UNI);
+    const uint32_t k = (uint32_t)iv[I_UK]++;
+    const uint64_t key = (((uint64_t)it << 32) | (k >> 1)) + 1;
+    if ((k & 1) && key == u_key) return u53(u_odd);
+    const u64x2 r = philox(A.seed, rid, it, k >> 1, TAG_UNI);
+    u_odd = r.b;
+    u_key = key;
+    return u53((k & 1) ? r.b : r.a);
   }
   __device__ __forceinline__ void sample_momentum(uint32_t c1, uint32_t c2hi, uint32_t tag) {
 #pragma unroll
@@ -427,7 +459,7 @@ struct NutsChain {
         }
         A.stats[((size_t)shard * A.S_total + col) * N_STATS + lane] = v;
       }
-      if (iv[I_DIV] && lane == 0) A.cnt[(size_t)gid * C_COUNT + C_DIV] += 1;
+      if (iv[I_DIV]) ++ndiv;
     }
     bool update = false;
     if (A.adapt && it < A.num_warmup) {
@@ -488,7 +520,7 @@ struct NutsChain {
 
   __device__ __forceinline__ bool on_leaf(double lp, const double (&glp)[NCH], int pause_at) {
     finish_leapfrog(lp, glp);
-    if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_LEAP] += 1;
+    ++nleap;
     const double H0 = s[S_H0];
     double h = s[S_V] + kinetic(p);
     if (isnan(h)) h = INFINITY;
@@ -715,6 +747,7 @@ __global__ __launch_bounds__(64) void k_nuts_step(NutsArgs A, int step_id, int p
     req = ch.consume(A.lp_in[gid], glp, pause_at);
   }
   ch.save();
+  ch.flush_counts();
   if (req) {
     ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);
     A.req_step[ch.shard] = step_id;
@@ -738,9 +771,11 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   const bool live = gid < A.nchains;
   extern __shared__ double fl_all[];
   const size_t nv = (size_t)V_COUNT * A.Dp, ns = (size_t)A.max_depth * stack_vecs(A) * A.Dp;
-  double* const fl = fl_all + (size_t)seg * (nv + ns);
+  const size_t nss = (size_t)A.max_depth * SS_COUNT;
+  double* const fl = fl_all + (size_t)seg * (nv + ns + nss);
   double* const gvec = A.vec + (size_t)gid * nv;
   double* const gstk = A.stk + (size_t)gid * A.max_depth * SV_COUNT * A.Dp;   // (allocation stride; ns used)
+  double* const gstks = A.stks + (size_t)gid * nss;
   bool run = live;
   if (run) {
     const int mode0 = A.iv[(size_t)gid * I_COUNT + I_MODE];
@@ -749,11 +784,14 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   if (run) {
     for (size_t i = lane; i < nv; i += SEG) fl[i] = gvec[i];
     for (size_t i = lane; i < ns; i += SEG) fl[nv + i] = gstk[i];
+    for (size_t i = lane; i < nss; i += SEG) fl[nv + ns + i] = gstks[i];
   }
   __syncthreads();
   if (run) {
-    NutsChain<NCH, SEG> ch(A, gid, lane, fl, fl + nv);
+    NutsChain<NCH, SEG> ch(A, gid, lane, fl, fl + nv, fl + nv + ns);
     ch.load();
+    double yc[NCH], sc[NCH];
+    schools_data<NCH, SEG>(ch.sh, yc, sc, lane, ch.D);
     const int mode = ch.iv[I_MODE];
     bool req = false, go = true;
     if (mode == M_PAUSED) {
@@ -772,12 +810,13 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
       unsigned long long ngrad = 0;
       while (req && steps < max_steps) {
         double glp[NCH];
-        const double lp = schools_lpgrad<NCH, SEG>(ch.sh, ch.q, glp, lane, ch.D);
+        const double lp = schools_lpgrad<NCH, SEG>(yc, sc, ch.q, glp, lane, ch.D);
         ++steps;
         req = ch.consume(lp, glp, pause_at);
         if (req) ++ngrad;
       }
       ch.save();
+      ch.flush_counts();
       if (req) ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);
       if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += ngrad;
     } else {
@@ -788,6 +827,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   if (run) {
     for (size_t i = lane; i < nv; i += SEG) gvec[i] = fl[i];
     for (size_t i = lane; i < ns; i += SEG) gstk[i] = fl[nv + i];
+    for (size_t i = lane; i < nss; i += SEG) gstks[i] = fl[nv + ns + i];
   }
 }
 
@@ -803,7 +843,9 @@ __global__ __launch_bounds__(64) void k_schools_lpgrad(const ShardDev* shards, i
     const int e = k * WAVE + lane;
     qq[k] = e < sh.D ? q[(size_t)c * Dp + e] : 0.0;
   }
-  const double v = schools_lpgrad<NCH>(sh, qq, gl, lane, sh.D);
+  double yc[NCH], sc[NCH];
+  schools_data<NCH>(sh, yc, sc, lane, sh.D);
+  const double v = schools_lpgrad<NCH>(yc, sc, qq, gl, lane, sh.D);
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int e = k * WAVE + lane;
@@ -824,7 +866,8 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
 }
 template <int NCH, int CPW, int MINW = 1>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
-  const size_t lds = CPW * sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp);
+  const size_t lds = CPW * sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp +
+                                             (size_t)A.max_depth * SS_COUNT);
   if (lds > 64 * 1024) {
     // the attribute is per device (allow_big_lds keys it on the current one); a failure is
     // reported as such rather than as a generic launch failure

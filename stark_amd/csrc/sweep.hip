@@ -1225,11 +1225,33 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   const double* xs = reinterpret_cast<const double*>(slot);
   const double* brow = bimg + lr * KB + lh * KF;
 
+  // ER = 2: the forward operands of sub-tile k+1 are read from the slot during sub-tile k's
+  // backward (their DMA was issued at the top of sub-tile k), the rest of the slot at the top of
+  // sub-tile k+1, which then releases it: the DMA flies during forward + residual + backward
+  static_assert(ER != 2 || IL == 0, "ER = 2 keeps the unsplit backward");
+  double fa2[ER == 2 ? KF : 1];
+  auto load_fa2 = [&]() {
+    const double* xr_ = xs + lr * d;
+#pragma unroll
+    for (int s = 0; s < KF; ++s) fa2[s] = xr_[std::min(lh * KF + s, d - 1)];
+  };
   if (mine > 0) issue(0);
   if (PF && mine > 1) touch(1);
+  if constexpr (ER == 2) {
+    if (mine > 0) {
+      __builtin_amdgcn_s_waitcnt(0xF70);
+      __builtin_amdgcn_sched_barrier(0);
+      load_fa2();
+    }
+  }
   for (int k = 0; k < mine; ++k) {
-    if (PF && k + 1 < mine) wait_vmcnt(npf);             // sub-tile k landed, the touches of k+1 may fly
-    else __builtin_amdgcn_s_waitcnt(0xF70);              // vmcnt(0): sub-tile k landed
+    if constexpr (ER == 2) {
+      // sub-tile k landed at the end of the previous iteration (or in the prologue)
+    } else if (PF && k + 1 < mine) {
+      wait_vmcnt(npf);                                   // sub-tile k landed, the touches of k+1 may fly
+    } else {
+      __builtin_amdgcn_s_waitcnt(0xF70);                 // vmcnt(0): sub-tile k landed
+    }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(2);
     const int rv = std::min(SM_R, nrows - SM_R * (w + NW * k));
@@ -1240,9 +1262,12 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
     if constexpr (R2) ea[0] = dbl4{alpha, alpha, alpha, alpha};     // D layout: lane holds chain lr
     double fa[ER ? KF : 1];
     const double* xrow = xs + lr * d;
-    if constexpr (ER) {
+    if constexpr (ER == 1) {
 #pragma unroll
       for (int s = 0; s < KF; ++s) fa[s] = xrow[std::min(lh * KF + s, d - 1)];
+    } else if constexpr (ER == 2) {
+#pragma unroll
+      for (int s = 0; s < KF; ++s) fa[s] = fa2[s];
     } else if constexpr (!(ABL & 4)) {
 #pragma unroll
       for (int s = 0; s < KF; ++s) ea[s % NACC] = mfma_f64(xrow[std::min(lh * KF + s, d - 1)], brow[s], ea[s % NACC]);
@@ -1382,7 +1407,16 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
       __builtin_amdgcn_s_setprio(0);
     }
     // ---- backward
-    if constexpr (!(ABL & 2)) {
+    if constexpr (ER == 2) {
+      if constexpr (!(ABL & 2)) bwd_rows(0, 2);
+      if (k + 1 < mine) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xF70);               // vmcnt(0): sub-tile k+1 landed
+        __builtin_amdgcn_sched_barrier(0);
+        load_fa2();
+      }
+      if constexpr (!(ABL & 2)) bwd_rows(2, 4);
+    } else if constexpr (!(ABL & 2)) {
       if (!bwd_done) bwd_rows(0, 4);
     }
   }
@@ -1445,7 +1479,6 @@ constexpr int G5_C = 64;      // chains (4 MFMA N tiles)
 constexpr int G5_KC = 32;     // pass F: columns per stage
 constexpr int G5_TR = 64;     // pass F: rows per tile (16 per wave)
 constexpr int G5_RB = 32;     // pass B: rows per stage
-constexpr int G5_STAGE = 32 * 1024;   // bytes per stage (A image + B image)
 
 __host__ __device__ inline int g5_kp(int d) { return (d + G5_KC - 1) / G5_KC * G5_KC; }
 // byte offset of element (row r, chain c) in a 512-B-row chain image (beta^T rows k, R rows r)
@@ -1467,11 +1500,10 @@ __global__ __launch_bounds__(256) void k_qt_swizzle(SweepArgs A, int d) {
 // Both passes: one block of G5_NW = 8 waves per CU (two per SIMD); wave w takes row / column
 // group w & 3 (16 rows or columns) and chain half w >> 2 (two 16-chain MFMA tiles), so every
 // output's K terms are summed in the same order as with one wave per group.  The stages run
-// through a ring of G5_NS = 4 LDS slots (128 KB): three stages are in flight while one is
+// through a ring of 4 LDS slots (128 KB): three stages are in flight while one is
 // consumed, and one barrier per stage both publishes the landed stage and frees the slot read
 // in the previous one (the refill of that slot is issued right after it).
 constexpr int G5_NW = 8;
-constexpr int G5_NS = 4;
 // A barrier that leaves LDS-DMAs in flight: __syncthreads() makes hipcc drain vmcnt(0) first
 // (an LDS-DMA is a pending LDS write on the VM counter), which would empty the stage ring at
 // every stage; the counted wait before it is what orders the DMA'd data.
@@ -1479,7 +1511,6 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);                   // lgkmcnt(0): this wave's LDS accesses done
   __builtin_amdgcn_s_barrier();
 }
-constexpr int G5_DMA = 4;     // DMA instructions per wave per stage (2 for each operand image)
 #ifndef G5_FW
 #define G5_FW 4               // pass F: waves per block (4: two blocks per CU)
 #endif
