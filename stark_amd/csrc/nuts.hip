@@ -162,6 +162,25 @@ __device__ __forceinline__ void write_draw(const NutsArgs& A, const ShardDev& sh
   if (lane == 0) out[(size_t)(sh.P - 1) * S + col] = lp;
 }
 
+// Cold paths of a transition's end, out of line: their transcendentals (Box-Muller's log / sqrt /
+// sin / cos, dual averaging's pow / exp / sqrt) would otherwise add their temporaries to the
+// register budget of the per-leapfrog loop they are inlined into.
+__device__ __noinline__ double momentum_cold(uint64_t seed, uint32_t rid, uint32_t c1, uint32_t c2hi, uint32_t e,
+                                             uint32_t tag, double im) {
+  return normal_at(seed, rid, c1, c2hi, e, tag) / sqrt(im);
+}
+struct DaState { double sbar, xbar, nomeps; };
+__device__ __noinline__ DaState dual_averaging_cold(double cnt, double sbar, double xbar, double mu, double adapt_stat,
+                                                   double t0, double delta, double gamma, double kappa) {
+  adapt_stat = adapt_stat > 1 ? 1 : adapt_stat;
+  const double eta = 1.0 / (cnt + t0);
+  sbar = (1.0 - eta) * sbar + eta * (delta - adapt_stat);
+  const double x = mu - sbar * sqrt(cnt) / gamma;
+  const double x_eta = pow(cnt, -kappa);
+  xbar = (1.0 - x_eta) * xbar + x_eta * x;
+  return DaState{sbar, xbar, exp(x)};
+}
+
 // ------------------------------------------------------------------ the chain
 // SEG: lanes per chain (64: one chain per wave; 16 / 32: 4 / 2 chains packed in a wave, each
 // in its own DPP row(s), D <= SEG).  `lane` is the lane's position inside its segment.
@@ -281,7 +300,7 @@ struct NutsChain {
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       const int e = k * SEG + lane;
-      p[k] = ok(k) ? normal_at(A.seed, rid, c1, c2hi, (uint32_t)e, tag) / sqrt(im[k]) : 0.0;
+      p[k] = ok(k) ? momentum_cold(A.seed, rid, c1, c2hi, (uint32_t)e, tag, im[k]) : 0.0;
     }
   }
   __device__ __forceinline__ void load_sample_point() {
@@ -326,13 +345,11 @@ struct NutsChain {
   // ---- adaptation (stepsize_adaptation, windowed var_adaptation)
   __device__ __forceinline__ void learn_stepsize(double adapt_stat) {
     s[S_DA_CNT] += 1.0;
-    adapt_stat = adapt_stat > 1 ? 1 : adapt_stat;
-    const double eta = 1.0 / (s[S_DA_CNT] + A.t0);
-    s[S_SBAR] = (1.0 - eta) * s[S_SBAR] + eta * (A.delta - adapt_stat);
-    const double x = s[S_MU] - s[S_SBAR] * sqrt(s[S_DA_CNT]) / A.gamma;
-    const double x_eta = pow(s[S_DA_CNT], -A.kappa);
-    s[S_XBAR] = (1.0 - x_eta) * s[S_XBAR] + x_eta * x;
-    s[S_NOMEPS] = exp(x);
+    const DaState r = dual_averaging_cold(s[S_DA_CNT], s[S_SBAR], s[S_XBAR], s[S_MU], adapt_stat, A.t0, A.delta,
+                                          A.gamma, A.kappa);
+    s[S_SBAR] = r.sbar;
+    s[S_XBAR] = r.xbar;
+    s[S_NOMEPS] = r.nomeps;
   }
   __device__ __forceinline__ bool learn_variance() {
     const unsigned cnt = (unsigned)iv[I_WCNT];
