@@ -136,32 +136,6 @@ __device__ double schools_lpgrad(const double (&yc)[NCH], const double (&sc)[NCH
   return lp;
 }
 
-// Constrained output row (extract() order: params, transformed params, lp__).
-template <int NCH, int SEG = WAVE>
-__device__ __forceinline__ void write_draw(const NutsArgs& A, const ShardDev& sh, int shard, int col, const double (&q)[NCH],
-                           double lp, int lane) {
-  double* out = A.draws + (size_t)shard * A.Pmax * A.S_total;
-  const int D = sh.D;
-  const size_t S = (size_t)A.S_total;
-  if (A.family == STK_SCHOOLS) {
-    const double mu = seg_bcast<SEG>(q[0], 0);
-    const double tau = exp(seg_bcast<SEG>(q[0], 1));
-#pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      const int e = k * SEG + lane;
-      if (e < D) out[(size_t)e * S + col] = (e == 1) ? tau : q[k];
-      if (e >= 2 && e < D) out[(size_t)(D + e - 2) * S + col] = mu + tau * q[k];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      const int e = k * SEG + lane;
-      if (e < D) out[(size_t)e * S + col] = (A.family == STK_LINREG && e == D - 1) ? exp(q[k]) : q[k];
-    }
-  }
-  if (lane == 0) out[(size_t)(sh.P - 1) * S + col] = lp;
-}
-
 // Cold paths of a transition's end, out of line: their transcendentals (Box-Muller's log / sqrt /
 // sin / cos, dual averaging's pow / exp / sqrt) would otherwise add their temporaries to the
 // register budget of the per-leapfrog loop they are inlined into.
@@ -169,6 +143,8 @@ __device__ __noinline__ double momentum_cold(uint64_t seed, uint32_t rid, uint32
                                              uint32_t tag, double im) {
   return normal_at(seed, rid, c1, c2hi, e, tag) / sqrt(im);
 }
+__device__ __noinline__ double exp_cold(double x) { return exp(x); }
+__device__ __noinline__ double log_cold(double x) { return log(x); }
 struct DaState { double sbar, xbar, nomeps; };
 __device__ __noinline__ DaState dual_averaging_cold(double cnt, double sbar, double xbar, double mu, double adapt_stat,
                                                    double t0, double delta, double gamma, double kappa) {
@@ -179,6 +155,32 @@ __device__ __noinline__ DaState dual_averaging_cold(double cnt, double sbar, dou
   const double x_eta = pow(cnt, -kappa);
   xbar = (1.0 - x_eta) * xbar + x_eta * x;
   return DaState{sbar, xbar, exp(x)};
+}
+
+// Constrained output row (extract() order: params, transformed params, lp__).
+template <int NCH, int SEG = WAVE>
+__device__ __forceinline__ void write_draw(const NutsArgs& A, const ShardDev& sh, int shard, int col, const double (&q)[NCH],
+                           double lp, int lane) {
+  double* out = A.draws + (size_t)shard * A.Pmax * A.S_total;
+  const int D = sh.D;
+  const size_t S = (size_t)A.S_total;
+  if (A.family == STK_SCHOOLS) {
+    const double mu = seg_bcast<SEG>(q[0], 0);
+    const double tau = exp_cold(seg_bcast<SEG>(q[0], 1));
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int e = k * SEG + lane;
+      if (e < D) out[(size_t)e * S + col] = (e == 1) ? tau : q[k];
+      if (e >= 2 && e < D) out[(size_t)(D + e - 2) * S + col] = mu + tau * q[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int e = k * SEG + lane;
+      if (e < D) out[(size_t)e * S + col] = (A.family == STK_LINREG && e == D - 1) ? exp_cold(q[k]) : q[k];
+    }
+  }
+  if (lane == 0) out[(size_t)(sh.P - 1) * S + col] = lp;
 }
 
 // ------------------------------------------------------------------ the chain
@@ -489,17 +491,17 @@ struct NutsChain {
       if (start_probe()) return true;
       finish_window_update();
     } else if (A.adapt && it + 1 == A.num_warmup) {
-      s[S_NOMEPS] = exp(s[S_XBAR]);   // complete_adaptation
+      s[S_NOMEPS] = exp_cold(s[S_XBAR]);   // complete_adaptation
     }
     return continue_or_stop(pause_at);
   }
 
   __device__ __forceinline__ void finish_window_update() {
-    s[S_MU] = log(10.0 * s[S_NOMEPS]);
+    s[S_MU] = log_cold(10.0 * s[S_NOMEPS]);
     s[S_DA_CNT] = 0.0;
     s[S_SBAR] = 0.0;
     s[S_XBAR] = 0.0;
-    if (iv[I_SSREASON] == 2) s[S_NOMEPS] = exp(s[S_XBAR]);
+    if (iv[I_SSREASON] == 2) s[S_NOMEPS] = exp_cold(s[S_XBAR]);
   }
 
   __device__ __forceinline__ bool on_probe(double lp, const double (&glp)[NCH], int pause_at) {
@@ -931,7 +933,11 @@ hipError_t stk_launch_nuts_fused(const NutsArgs& A, int nch, int pause_at, int m
   if (nch == 1) {
     switch (fused_cpw(A)) {
       case 4: return launch_fused_t<1, 4>(A, pause_at, max_steps, st);
+#ifdef STK_FUSED_MINW2   // measurement builds only (tools/gpu): chains_per_wave = 2 at two waves per SIMD
+      case 2: return launch_fused_t<1, 2, 2>(A, pause_at, max_steps, st);
+#else
       case 2: return launch_fused_t<1, 2>(A, pause_at, max_steps, st);
+#endif
       default: return launch_fused_t<1, 1>(A, pause_at, max_steps, st);
     }
   }
