@@ -139,9 +139,15 @@ __device__ double schools_lpgrad(const double (&yc)[NCH], const double (&sc)[NCH
 // Cold paths of a transition's end, out of line: their transcendentals (Box-Muller's log / sqrt /
 // sin / cos, dual averaging's pow / exp / sqrt) would otherwise add their temporaries to the
 // register budget of the per-leapfrog loop they are inlined into.
+// (normal_at's Box-Muller with one sincos: lanes of even and odd e share a wave, so a sin / cos
+// branch would run both functions under complementary masks)
 __device__ __noinline__ double momentum_cold(uint64_t seed, uint32_t rid, uint32_t c1, uint32_t c2hi, uint32_t e,
                                              uint32_t tag, double im) {
-  return normal_at(seed, rid, c1, c2hi, e, tag) / sqrt(im);
+  const u64x2 r = philox(seed, rid, c1, c2hi | (e >> 1), tag);
+  const double rad = sqrt(-2.0 * log(u53(r.a)));
+  double sn, cs;
+  sincos(6.283185307179586 * u53(r.b), &sn, &cs);
+  return ((e & 1) ? rad * sn : rad * cs) / sqrt(im);
 }
 __device__ __noinline__ double exp_cold(double x) { return exp(x); }
 __device__ __noinline__ double log_cold(double x) { return log(x); }

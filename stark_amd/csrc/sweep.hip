@@ -1556,7 +1556,7 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
   extern __shared__ __attribute__((aligned(16))) double lds[];
   char* const stg = reinterpret_cast<char*>(lds);                 // NS stages of STG bytes
   double* const sptab = reinterpret_cast<double*>(stg + NS * STG);
-  if constexpr (FAM == STK_LOGREG) logit_tables_init(sptab);
+  if constexpr (FAM == STK_LOGREG) logit3_tables_init(sptab);
 
   // per-lane chain constants: chain 16 ct + lr, ct = 2 wc + c2
   const double* qb = A.q + (size_t)shard * G5_C * A.Dp;
@@ -1656,7 +1656,7 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
           const double eta = *eslot(e) + al;
           double dv, lt;
           if constexpr (FAM == STK_LOGREG) {
-            logit_resid(eta, yv == 0.0 ? 0x80000000u : 0u, sptab, lt, dv);
+            logit_resid3(eta, yv == 0.0 ? 0x80000000u : 0u, sptab, lt, dv);
           } else {
             const double z = (yv - eta) * isg;
             lt = z * z;
@@ -1911,7 +1911,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *T = G5_TR;
     *LD = 0;
     *G = (int)g;
-    *lds_bytes = G5_FS * g5_fstage_bytes() + LG_TAB * sizeof(double);
+    *lds_bytes = G5_FS * g5_fstage_bytes() + LG3_TAB * sizeof(double);
     return;
   }
   if (var == 4) {
