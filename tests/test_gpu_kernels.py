@@ -371,3 +371,20 @@ def test_fullsize_shards_sum_to_full_data(ctx):
         scale = np.abs(g1[c]).max() + 1.0
         assert np.all(np.abs(g8[c] - g1[c]) <= RTOL_LP * np.maximum(np.abs(g1[c]), scale * 1e-3)), \
             (c, np.abs(g8[c] - g1[c]).max(), scale)
+
+
+def test_c_abi_rejects_bad_bernoulli_y(ctx):
+    """stk_model_create (the boundary a reference-side binding calls directly, without the
+    Python wrapper's check) rejects a logistic y outside {0, 1}: the sweeps read y as a sign bit."""
+    import ctypes
+    from stark_amd import _lib, engine
+    x = np.zeros((5, 3))
+    y = np.array([0, 1, 2, 1, 0], np.int32)
+    arr = (engine.Shard * 1)()
+    arr[0] = engine.Shard(5, 3, x.ctypes.data, None, y.ctypes.data, None)
+    h = ctypes.c_void_p()
+    rc = _lib.load().stk_model_create(ctx._h, engine.STK_LOGREG, arr, 1, ctypes.byref(h))
+    assert rc != 0 and "y_int[2] = 2" in _lib.load().stk_last_error().decode()
+    y[2] = 1
+    assert _lib.load().stk_model_create(ctx._h, engine.STK_LOGREG, arr, 1, ctypes.byref(h)) == 0
+    _lib.load().stk_model_destroy(h)
