@@ -560,9 +560,11 @@ def main():
         "combine": {"gpu_ms": float(np.median(comb_ms[1:])), "gpu_ms_min": min(comb_ms[1:]),
                     "gpu_ms_first_call": comb_ms[0], "host_buffers_ms": comb_host_ms, "shards": a.shards, "P": P,
                     "draws": C * n_post, "all_gather_ms": 1e3 * t_gather,
-                    "note": "engine.consensus(separate_lp=True) on the all-gathered DEVICE draws (no host copy), the "
-                            "result left in HBM; wall time of the call (median of 5 after the first); host_buffers_ms: "
-                            "the same combine through host numpy buffers (H2D + D2H copies included)"},
+                    "draws_on_device": bool(getattr(allp_dev, "is_cuda", False)),
+                    "note": "engine.consensus(separate_lp=True) on the all-gathered draws where they lie (device "
+                            "draws from RCCL: no host copy, the result left in HBM; a gloo rehearsal gathers on the "
+                            "host); wall time of the call (median of 5 after the first); host_buffers_ms: the same "
+                            "combine through host numpy buffers (H2D + D2H copies included)"},
         "setup_s": {"datagen": t_gen, "adaptation": t_adapt, "post_warmup_draws": t_post},
         "timed_window_monotonic_ns": [w0, w1],     # tools/rocpd_summary.py window: the kernel trace's dispatches in it
         "divergent": info["divergent"],

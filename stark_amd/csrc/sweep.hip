@@ -875,6 +875,9 @@ __device__ void logit3_tables_init(double* tab) {
   }
 }
 
+// NEWTON: one Newton step on v_rcp_f64 (measurement variants drop it: tools/rcp_acc.hip);
+// EXP4: degree-4 Taylor exp (else a fitted degree 3, relative error 7e-14)
+template <bool NEWTON = true, bool EXP4 = true>
 __device__ __forceinline__ void logit_resid3(double eta, uint32_t ymask, const double* tab, double& lt, double& dv) {
   constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
   constexpr double INV_L = 369.3299304675746;             // 256 / ln 2
@@ -889,7 +892,8 @@ __device__ __forceinline__ void logit_resid3(double eta, uint32_t ymask, const d
   const double n = sn - MAGIC;
   double r = fma(-n, L_HI, -a);
   r = fma(-n, L_LO, r);
-  const double p = fma(fma(fma(fma(1.0 / 24.0, r, 1.0 / 6.0), r, 0.5), r, 1.0), r, 1.0);
+  const double p = EXP4 ? fma(fma(fma(fma(1.0 / 24.0, r, 1.0 / 6.0), r, 0.5), r, 1.0), r, 1.0)
+                        : fma(fma(fma(0.16666667813799327, r, 0.500000038186625), r, 1.0), r, 1.0);
   const double e = __builtin_amdgcn_ldexp(tab[ni & 255] * p, ni >> 8);
   const int j = (int)fma(e, 256.0, 0.5);                  // rint(256 e), e in [0, 1] (v_cvt_i32_f64 truncates)
   const double* cj = tab + 256 + 4 * j;
@@ -899,7 +903,7 @@ __device__ __forceinline__ void logit_resid3(double eta, uint32_t ymask, const d
   const double lg = fma(rl, q, cj[2]);
   const double u = 1.0 + e;
   double ri = __builtin_amdgcn_rcp(u);
-  ri = fma(ri, fma(-u, ri, 1.0), ri);
+  if constexpr (NEWTON) ri = fma(ri, fma(-u, ri, 1.0), ri);
   const double w = e * ri;
   const uint32_t neg = (uint32_t)((int32_t)(__builtin_bit_cast(uint64_t, t) >> 32) >> 31);   // ~0u when t < 0
   const double dvp = blend(neg, ri, w);
@@ -1171,11 +1175,11 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
   double* const bimg = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);  // [16][KB]
   double* const sptab = bimg + C * KB;
   // ER: the 4 remainder columns (16 rows x 4) of the wave's sub-tile, kept past the slot's release
-  constexpr int TABN = RV == 3 ? LG3_TAB : LG_TAB;
+  constexpr int TABN = RV >= 3 ? LG3_TAB : LG_TAB;
   double* const xst = sptab + TABN + w * 64;
   double* const pfd = sptab + TABN + NW * 64 + w * 32;       // PF: 256-B dummy per wave
   constexpr bool R2 = FAM == STK_LOGREG && RV >= 2;
-  if constexpr (FAM == STK_LOGREG && RV == 3) logit3_tables_init(sptab);
+  if constexpr (FAM == STK_LOGREG && RV >= 3) logit3_tables_init(sptab);
   else if constexpr (R2) logit_tables_init(sptab);
   else if constexpr (FAM == STK_LOGREG) softplus_tables_init(sptab);
   const double* qs = A.q + (size_t)shard * C * A.Dp;
@@ -1354,7 +1358,7 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
 #pragma unroll
           for (int i = i0; i < i1; ++i) {
             double lt;
-            if constexpr (RV == 3) logit_resid3(eta4[i], ym[i], sptab, lt, de[i]);
+            if constexpr (RV >= 3) logit_resid3<RV == 3, RV != 5>(eta4[i], ym[i], sptab, lt, de[i]);
             else logit_resid(eta4[i], ym[i], sptab, lt, de[i]);
             lpa += lt;
             gaa += de[i];
@@ -1367,7 +1371,7 @@ __global__ __launch_bounds__(256, 2) void k_sweepe(SweepArgs A) {
         for (int i = 0; i < 4; ++i) {
           const bool valid = lh + 4 * i < rv;
           double lt, dv;
-          if constexpr (RV == 3) logit_resid3(eta4[i], ym[i], sptab, lt, dv);
+          if constexpr (RV >= 3) logit_resid3<RV == 3, RV != 5>(eta4[i], ym[i], sptab, lt, dv);
           else logit_resid(eta4[i], ym[i], sptab, lt, dv);
           dv = valid ? dv : 0.0;
           lpa += valid ? lt : 0.0;
