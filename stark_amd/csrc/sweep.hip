@@ -875,8 +875,10 @@ __device__ void logit3_tables_init(double* tab) {
   }
 }
 
-// NEWTON: one Newton step on v_rcp_f64 (measurement variants drop it: tools/rcp_acc.hip);
-// EXP4: degree-4 Taylor exp (else a fitted degree 3, relative error 7e-14)
+// NEWTON: one Newton step on v_rcp_f64, which alone is good to ~2^-24 only (tools/rcp_acc.hip,
+// profiles/r03s_rcp_acc.log: 2.6e8 ulp; 11 ulp after the step); without it the gradient moves by
+// 4e-9 relative (RV 4, measurement only).  EXP4: degree-4 Taylor exp (else a fitted degree 3,
+// relative error 7e-14; RV 5, measurement only: no faster, profiles/r03s_sweepe_ab.log).
 template <bool NEWTON = true, bool EXP4 = true>
 __device__ __forceinline__ void logit_resid3(double eta, uint32_t ymask, const double* tab, double& lt, double& dv) {
   constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
