@@ -1,7 +1,8 @@
 // Measurement-only variants of the 16-chain sweep ("tried and measured"):
 // k_sweepr (the next sub-tile streamed through VGPRs), k_sweepq and k_sweepx (the 4x4x4
-// four-block fp64 MFMA).  Each was correct and slower than k_sweepe; they are kept here, out of
-// libstark_hip.so, for tools/sweep_micro.hip only (included after sweep.hip, namespace stk).
+// four-block fp64 MFMA), k_sweepw (one wave per SIMD, software-pipelined).  Each was correct
+// and slower than k_sweepe; they are kept here, out of libstark_hip.so, for tools/sweep_micro.hip
+// and tools/sweepe_ab.hip only (included after sweep.hip, namespace stk).
 // Build: see tools/sweep_micro.hip.
 namespace stk {
 
@@ -649,6 +650,243 @@ static size_t sweepq_lds(int S, int NB, int KF, int d) {
   const size_t ring = (size_t)SM_W * NB * sweepq_slot_bytes(S, d) + SP_TAB * sizeof(double);
   const size_t red = ((size_t)SM_W * 4 * KF * 16 + (size_t)SM_W * 64 * 2) * sizeof(double);
   return std::max(ring, red);
+}
+
+// v4w (tools/sweepe_ab.hip; measured 17.6 ms against k_sweepe's 14.7 on one box, MFMA busy 48 %
+// at 2.2 GHz against 71 % at 1.8: one wave per SIMD does not keep the fp64 pipe fed, as with
+// k_sweepf in round 2 -- profiles/r03t_*): k_sweepe's arithmetic at ONE wave per SIMD
+// (one 256-thread block per CU), software-pipelined so the wave itself keeps the fp64 pipe busy:
+// two LDS slots per wave (the DMA of sub-tile k+2 is issued at the top of sub-tile k, a whole
+// iteration before it is needed), beta's B fragments in registers (the wave has 512), and per
+// iteration
+//   phase A: the residual of sub-tile k (VALU)  interleaved with  the forward of sub-tile k+1 (MFMA)
+//   phase B: the backward of sub-tile k (MFMA)  interleaved with  the reads of sub-tile k+1's
+//            backward operands, y and remainder columns from its slot (LDS)
+// with the backward operands double-buffered in registers by sub-tile parity.
+template <int FAM, int KF, int JT, int AUX = 2, int SGB = 1>
+__global__ __launch_bounds__(256, 1) void k_sweepw(SweepArgs A) {
+  constexpr int C = SM_C, NW = SM_W, JTV = JT - 1;
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + 63) / 64;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * 64, r1 = std::min<int64_t>(sh.n, t1 * 64);
+  const int nrows = (int)(r1 - r0);
+  const int nsub = (nrows + SM_R - 1) / SM_R;
+  const int mine = nsub > w ? (nsub - w + NW - 1) / NW : 0;
+  constexpr int YB = (FAM == STK_LOGREG) ? 4 : 8;
+  const int SBX = SM_R * d * 8;
+  const int SS = sweepm_slot_bytes(d);
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const slots = reinterpret_cast<char*>(lds) + (size_t)w * 2 * SS;
+  double* const sptab = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * 2 * SS);
+  if constexpr (FAM == STK_LOGREG) logit3_tables_init(sptab);
+  const double* qc = A.q + ((size_t)shard * C + lr) * A.Dp;
+  double bf[KF];
+#pragma unroll
+  for (int s = 0; s < KF; ++s) {
+    const int col = lh * KF + s;
+    bf[s] = col < d ? qc[1 + col] : 0.0;
+  }
+  const double alpha = qc[0];
+  const double inv_s = (FAM == STK_LINREG) ? exp(-qc[d + 1]) : 0.0;
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0xF70);
+
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
+  const void* ybase = (FAM == STK_LOGREG) ? (const void*)(sh.yi + r0) : (const void*)(sh.y + r0);
+  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(ybase, (int64_t)nrows * YB);
+  const int nx = (SBX + 1023) >> 10;
+  const int last_lanes = (SBX - ((nx - 1) << 10)) >> 4;
+  const int per_tile = nx + 1;
+  auto slot_of = [&](int k) { return slots + (size_t)(k & 1) * SS; };
+  auto issue = [&](int k) {
+    char* const sl = slot_of(k);
+    const int u = w + NW * k;
+    const int xoff = u * SBX;
+    for (int j = 0; j < nx - 1; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(sl + j * 1024), 16, lane * 16, xoff + j * 1024, 0, AUX);
+    if (lane < last_lanes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(sl + (nx - 1) * 1024), 16, lane * 16,
+                                               xoff + (nx - 1) * 1024, 0, AUX);
+    if (lane < SM_R * YB / 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_vptr)(sl + SBX), 4, lane * 4, u * SM_R * YB, 0, AUX);
+  };
+
+  dbl4 gacc[JTV];
+#pragma unroll
+  for (int t = 0; t < JTV; ++t) gacc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double gv[4] = {0.0, 0.0, 0.0, 0.0};
+  double lpa = 0.0, gaa = 0.0;
+  // per-sub-tile operands, double-buffered by parity
+  double xa[2][4][JTV];
+  dbl2 xv[2][4][2];
+  double yv[2][4];
+  uint32_t ym[2][4];
+  dbl4 eta = {0.0, 0.0, 0.0, 0.0};
+
+  auto forward = [&](int k) {                        // eta of sub-tile k, alpha in the accumulator
+    const double* xrow = reinterpret_cast<const double*>(slot_of(k)) + lr * d;
+    dbl4 e0 = FAM == STK_LOGREG ? dbl4{alpha, alpha, alpha, alpha} : dbl4{0.0, 0.0, 0.0, 0.0};
+    dbl4 e1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < KF; ++s) {
+      if (s & 1) e1 = mfma_f64(xrow[lh * KF + s], bf[s], e1);      // d == 4 KF (host-checked)
+      else e0 = mfma_f64(xrow[lh * KF + s], bf[s], e0);
+    }
+    return e0 + e1;
+  };
+  auto read_rest = [&](int k, auto P) {              // backward operands, remainder columns, y
+    constexpr int par = decltype(P)::value;
+    const char* sl = slot_of(k);
+    const double* xs = reinterpret_cast<const double*>(sl);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < JTV; ++t) xa[par][s][t] = xs[(lh + 4 * s) * d + 16 * t + lr];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const dbl2* pv = reinterpret_cast<const dbl2*>(xs + (lh + 4 * i) * d + 16 * JTV);
+      xv[par][i][0] = pv[0];
+      xv[par][i][1] = pv[1];
+      if constexpr (FAM == STK_LOGREG)
+        ym[par][i] = ((uint32_t)*reinterpret_cast<const int32_t*>(sl + SBX + (lh + 4 * i) * 4) << 31) + 0x80000000u;
+      else
+        yv[par][i] = *reinterpret_cast<const double*>(sl + SBX + (lh + 4 * i) * 8);
+    }
+  };
+
+  if (mine > 0) issue(0);
+  if (mine > 1) issue(1);
+  if (mine > 0) {
+    wait_vmcnt(mine > 1 ? per_tile : 0);
+    __builtin_amdgcn_sched_barrier(0);
+    eta = forward(0);
+    read_rest(0, std::integral_constant<int, 0>{});
+  }
+
+  auto body = [&](int k, auto P, auto M) {
+    constexpr int par = decltype(P)::value;
+    constexpr int nxt = par ^ 1;
+    constexpr bool more = decltype(M)::value;         // a sub-tile k+1 follows (the last one is peeled)
+    __builtin_amdgcn_s_waitcnt(0xC07F);                 // lgkmcnt(0): slot k fully read (last iteration)
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + 2 < mine) issue(k + 2);                     // into slot k's
+    if constexpr (more) wait_vmcnt(k + 2 < mine ? per_tile : 0);   // sub-tile k+1 landed
+    __builtin_amdgcn_sched_barrier(0);
+    const int rv = std::min(SM_R, nrows - SM_R * (w + NW * k));
+    // ---- phase A: residual of k, forward of k+1
+    double de[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool valid = lh + 4 * i < rv;
+      double lt, dv;
+      if constexpr (FAM == STK_LOGREG) {
+        logit_resid3(eta[i], ym[par][i], sptab, lt, dv);
+      } else {
+        const double z = (yv[par][i] - (eta[i] + alpha)) * inv_s;
+        lt = z * z;
+        dv = z * inv_s;
+      }
+      dv = valid ? dv : 0.0;
+      lpa += valid ? lt : 0.0;
+      gaa += dv;
+      de[i] = dv;
+    }
+    dbl4 eta_n = eta;
+    if constexpr (more) eta_n = forward(k + 1);
+    if constexpr (SGB && more) {
+#pragma unroll
+      for (int s = 0; s < KF; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);   // 6 VALU
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase B: backward of k, reads of k+1's operands
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < JTV; ++t) gacc[t] = mfma_f64(xa[par][s][t], de[s], gacc[t]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      gv[0] = fma(xv[par][i][0].x, de[i], gv[0]);
+      gv[1] = fma(xv[par][i][0].y, de[i], gv[1]);
+      gv[2] = fma(xv[par][i][1].x, de[i], gv[2]);
+      gv[3] = fma(xv[par][i][1].y, de[i], gv[3]);
+    }
+    if constexpr (more) read_rest(k + 1, std::integral_constant<int, nxt>{});
+    if constexpr (SGB && more) {
+#pragma unroll
+      for (int s = 0; s < 4 * JTV; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);   // 1 VALU
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    eta = eta_n;
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  int k = 0;
+  for (; k + 2 < mine; k += 2) {                      // pairs with a successor each
+    body(k, I0{}, T_{});
+    body(k + 1, I1{}, T_{});
+  }
+  if (k + 1 < mine) {                                 // two left: the second is the last
+    body(k, I0{}, T_{});
+    body(k + 1, I1{}, F_{});
+  } else if (k < mine) {                              // one left
+    body(k, I0{}, F_{});
+  }
+
+  // ---- fixed-order block reduction (as k_sweepe)
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __syncthreads();
+  double* red = lds;
+  constexpr int JC = JT * 16;
+#pragma unroll
+  for (int t = 0; t < JTV; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[((size_t)w * JC + 16 * t + lh + 4 * i) * 16 + lr] = gacc[t][i];
+  double* red2 = red + (size_t)NW * JC * 16;
+  red2[(size_t)tid * 2 + 0] = lpa;
+  red2[(size_t)tid * 2 + 1] = gaa;
+  double* red3 = red2 + (size_t)NW * 64 * 2;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) red3[((size_t)(w * 4 + lh) * 4 + jj) * 16 + lr] = gv[jj];
+  __syncthreads();
+  double* out = A.partial + ((size_t)shard * A.Gs + chunk) * C * A.PW;
+  const int jv = 16 * JTV;
+  for (int i = tid; i < C * d; i += NW * 64) {
+    const int c = i / d, j = i % d;
+    double v = 0.0;
+    if (j < jv) {
+      for (int ww = 0; ww < NW; ++ww) v += red[((size_t)ww * JC + j) * 16 + c];
+    } else {
+      for (int ww = 0; ww < NW; ++ww)
+        for (int h = 0; h < 4; ++h) v += red3[((size_t)(ww * 4 + h) * 4 + (j - jv)) * 16 + c];
+    }
+    out[(size_t)c * A.PW + 1 + j] = v;
+  }
+  if (tid < 2 * C) {
+    const int c = tid >> 1, kind = tid & 1;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww)
+      for (int h = 0; h < 4; ++h) v += red2[(size_t)(ww * 64 + h * 16 + c) * 2 + kind];
+    out[(size_t)c * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
 }
 
 }  // namespace stk

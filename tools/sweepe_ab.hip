@@ -8,6 +8,7 @@
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/sweepe_ab.hip -o tools/_bin/sweepe_ab
 // Run:   tools/_bin/sweepe_ab [rows_per_shard] [shards] [rounds] [reps]
 #include "../stark_amd/csrc/sweep.hip"
+#include "sweep_variants.hip"
 #include "../stark_amd/csrc/datagen.hip"
 #include <stdarg.h>
 #include <stdio.h>
@@ -79,22 +80,24 @@ int main(int argc, char** argv) {
   SweepArgs A{sh_d, q, partial, nullptr, 0, C, Dp, G, LD, d + 2, 0, G, nullptr};
   printf("rows/shard %lld shards %d d %d C %d: G %d lds %zu, %.1f GB per sweep\n", (long long)rows, nsh, d, C, G, lds,
          bytes / 1e9);
-  struct Arm { const char* name; const void* kern; std::vector<float> ms; };
+  struct Arm { const char* name; const void* kern; std::vector<float> ms; size_t lds = 0; };
+  const size_t lds_w = (size_t)SM_W * 2 * sweepm_slot_bytes(d) + LG3_TAB * sizeof(double);
   std::vector<Arm> arms = {
       {"e2er", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 2, 2, 1>, {}},
       {"e3-nt-p1", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 3, 2, 0, 2, 1>, {}},
-      {"e4-nt-p1", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 4, 2, 0, 2, 1>, {}},
-      {"e5-nt-p1", (const void*)k_sweepe<STK_LOGREG, 25, 7, 0, 5, 2, 0, 2, 1>, {}},
+      {"w-sgb", (const void*)k_sweepw<STK_LOGREG, 25, 7, 2, 1>, {}, lds_w},
+      {"w", (const void*)k_sweepw<STK_LOGREG, 25, 7, 2, 0>, {}, lds_w},
       {"e2-all-nt", (const void*)k_sweepe<STK_LOGREG, 25, 7, 7, 2, 2, 0, 2>, {}},
   };
   for (auto& a : arms) CK(hipFuncSetAttribute(a.kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  auto launch = [&](const void* k) {
-    hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(k)), dim3(nsh * G), dim3(256), lds, st, A);
+  auto launch = [&](const Arm& a) {
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.kern)), dim3(nsh * G), dim3(256),
+                       a.lds ? a.lds : lds, st, A);
   };
   // parity: every arm with arithmetic vs e2er after the chunk reduction
   std::vector<std::vector<double>> res;
   for (int k = 0; k < 4; ++k) {
-    launch(arms[k].kern);
+    launch(arms[k]);
     CK(hipGetLastError());
     CK(stk_launch_sweep_reduce(STK_LOGREG, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
     std::vector<double> h((size_t)nsh * C * (Dp + 1));
@@ -113,10 +116,10 @@ int main(int argc, char** argv) {
   }
   for (int r = 0; r < rounds; ++r) {
     for (auto& a : arms) {
-      launch(a.kern);
+      launch(a);
       CK(hipStreamSynchronize(st));
       CK(hipEventRecord(e0, st));
-      for (int i = 0; i < reps; ++i) launch(a.kern);
+      for (int i = 0; i < reps; ++i) launch(a);
       CK(hipEventRecord(e1, st));
       CK(hipEventSynchronize(e1));
       float ms;
