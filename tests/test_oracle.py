@@ -150,3 +150,22 @@ def test_oracle_transition_deterministic(orc):
     b = m.transition(q0, seed=5, gid=3, iteration=7, eps=0.3)
     np.testing.assert_array_equal(a[0], b[0])
     assert a[2][3] == 2 ** a[2][2] - 1 or a[2][4] == 1 or a[2][2] >= 0
+
+
+def test_residual_v3_emulation_accuracy():
+    """The design of k_sweepe's logistic residual v3 (tables, polynomial degrees, Stan's +-20
+    cutoffs by clamping, one Newton step on a 2^-24 reciprocal seed), emulated in numpy by
+    tools/residual_v3_accuracy.py, against Stan's bernoulli_logit term in long double: lt within
+    4e-15 absolute and dv within 1e-15 relative away from the cutoff bands, exactly Stan's (t, 1)
+    below -20, NaN kept.  (The GPU kernel is checked against the oracle in test_gpu_kernels.py.)"""
+    import numpy as np
+    from tools import residual_v3_accuracy as R
+    t = np.concatenate([np.random.default_rng(3).uniform(-25, 25, 100_000), np.linspace(-21, -19, 2001)])
+    lt, dv = R.resid3(t)
+    lr, dr = R.stan(t)
+    inner = np.abs(t) < 20
+    assert np.abs(lt - lr.astype(np.float64))[inner].max() < 4e-15
+    assert (np.abs(dv - dr.astype(np.float64)) / dr.astype(np.float64))[inner].max() < 1e-15
+    low = t < -20
+    assert np.array_equal(lt[low], t[low]) and np.all(dv[low] == 1.0)
+    assert np.isnan(R.resid3(np.array([np.nan]))[0][0])
