@@ -32,11 +32,13 @@ namespace stk {
 
 
 // Lane exchange of a double by DPP (VALU, a few cycles; __shfl is a ds_bpermute round trip).
+// bound_ctrl: an invalid source lane reads 0 -- the old value 0 would give the same, but as an
+// operand it costs a v_mov of 0 into the destination before every DPP move.
 template <int CTRL>
 __device__ __forceinline__ double nuts_dpp(double v) {
   const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, true);
   return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 // Lane l's double, as a wave-uniform (scalar) value.
@@ -75,11 +77,18 @@ __device__ __forceinline__ double seg_sum(double v) {
     return v;
   }
 }
-// Lane l of this lane's segment, broadcast to the segment.
-template <int SEG>
-__device__ __forceinline__ double seg_bcast(double v, int l) {
-  if constexpr (SEG == WAVE) return lane_d(v, l);
-  else return __shfl(v, ((int)threadIdx.x & (WAVE - SEG)) + l);
+// Lane L of this lane's segment, broadcast to the segment: a segment of 16 is one DPP row, so
+// row_newbcast (a VALU move) instead of a ds_bpermute round trip through the LDS crossbar.
+template <int SEG, int L>
+__device__ __forceinline__ double seg_bcast(double v) {
+  if constexpr (SEG == WAVE) {
+    return lane_d(v, L);
+  } else if constexpr (SEG == 16) {
+    static_assert(L >= 0 && L < 16, "row_newbcast selects a lane of the row");
+    return nuts_dpp<0x150 + L>(v);
+  } else {
+    return __shfl(v, ((int)threadIdx.x & (WAVE - SEG)) + L);
+  }
 }
 
 __device__ __forceinline__ double log_sum_exp2(double a, double b) {   // stan::math::log_sum_exp
@@ -108,8 +117,8 @@ __device__ __forceinline__ void schools_data(const ShardDev& sh, double (&yc)[NC
 template <int NCH, int SEG = WAVE>
 __device__ double schools_lpgrad(const double (&yc)[NCH], const double (&sc)[NCH], const double (&q)[NCH],
                                  double (&glp)[NCH], int lane, int D) {
-  const double mu = seg_bcast<SEG>(q[0], 0);
-  const double u = seg_bcast<SEG>(q[0], 1);
+  const double mu = seg_bcast<SEG, 0>(q[0]);
+  const double u = seg_bcast<SEG, 1>(q[0]);
   const double tau = exp(u);
   double lp = 0.0, smu = 0.0, su = 0.0;
 #pragma unroll
@@ -171,8 +180,8 @@ __device__ __forceinline__ void write_draw(const NutsArgs& A, const ShardDev& sh
   const int D = sh.D;
   const size_t S = (size_t)A.S_total;
   if (A.family == STK_SCHOOLS) {
-    const double mu = seg_bcast<SEG>(q[0], 0);
-    const double tau = exp_cold(seg_bcast<SEG>(q[0], 1));
+    const double mu = seg_bcast<SEG, 0>(q[0]);
+    const double tau = exp_cold(seg_bcast<SEG, 1>(q[0]));
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       const int e = k * SEG + lane;
@@ -204,6 +213,11 @@ struct NutsChain {
   double* const vec;
   double* const stk;
   double* const stks;
+  // the per-transition scalars and counters live in registers; the ones touched only at a
+  // transition's end or by adaptation (cold_s / cold_i) stay in memory -- the chain's global
+  // block, or its LDS image in the fused kernel -- and are read and written in place
+  double* const scold;
+  int* const icold;
   double s[S_COUNT];
   int iv[I_COUNT];
   double q[NCH], p[NCH], g[NCH], im[NCH];
@@ -211,17 +225,33 @@ struct NutsChain {
 
   __device__ __forceinline__ NutsChain(const NutsArgs& a, int gid_, int lane_)
       : NutsChain(a, gid_, lane_, a.vec + (size_t)gid_ * V_COUNT * a.Dp,
-                  a.stk + (size_t)gid_ * a.max_depth * SV_COUNT * a.Dp) {}
-  // vec_ / stk_ / stks_: this chain's vector block, tree stack and stack scalars (global memory,
-  // or LDS copies)
+                  a.stk + (size_t)gid_ * a.max_depth * SV_COUNT * a.Dp, a.stks + (size_t)gid_ * a.max_depth * SS_COUNT,
+                  a.sc + (size_t)gid_ * S_COUNT, a.iv + (size_t)gid_ * I_COUNT) {}
+  // vec_ / stk_ / stks_ / scold_ / icold_: this chain's vector block, tree stack, stack scalars
+  // and cold scalars / counters (global memory, or the fused kernel's LDS image).  No null
+  // defaults: a select between an LDS and a global pointer leaves a generic pointer, and every
+  // access through it a flat instruction (waits on both the vector-memory and the LDS counter)
   __device__ __forceinline__ NutsChain(const NutsArgs& a, int gid_, int lane_, double* vec_, double* stk_,
-                                       double* stks_ = nullptr)
+                                       double* stks_, double* scold_, int* icold_)
       : A(a), gid(gid_), lane(lane_), shard(gid_ / a.C), cidx(gid_ % a.C), D(a.shards[gid_ / a.C].D),
         rid(rng_stream(a, gid_)),
         sh(a.shards[gid_ / a.C]),
         vec(vec_),
         stk(stk_),
-        stks(stks_ ? stks_ : a.stks + (size_t)gid_ * a.max_depth * SS_COUNT) {}
+        stks(stks_),
+        scold(scold_),
+        icold(icold_) {}
+
+  static constexpr bool cold_s(int i) {
+    return i == S_VS || i == S_HS || i == S_NOMEPS || i == S_DA_CNT || i == S_SBAR || i == S_XBAR || i == S_MU ||
+           i == S_WFN || i == S_PH0;
+  }
+  static constexpr bool cold_i(int i) {
+    return i == I_PROBE || i == I_PDIR || i == I_SSCALL || i == I_SSREASON || i == I_WCNT || i == I_WSIZE ||
+           i == I_WNEXT;
+  }
+  __device__ __forceinline__ double& S(int i) { return cold_s(i) ? scold[i] : s[i]; }
+  __device__ __forceinline__ int& IV(int i) { return cold_i(i) ? icold[i] : iv[i]; }
 
   __device__ __forceinline__ bool ok(int k) const { return k * SEG + lane < D; }
   __device__ __forceinline__ double* vp(int v) const { return vec + (size_t)v * A.Dp; }
@@ -246,9 +276,11 @@ struct NutsChain {
     const double* sc = A.sc + (size_t)gid * S_COUNT;
     const int* ivp = A.iv + (size_t)gid * I_COUNT;
 #pragma unroll
-    for (int i = 0; i < S_COUNT; ++i) s[i] = sc[i];
+    for (int i = 0; i < S_COUNT; ++i)
+      if (!cold_s(i)) s[i] = sc[i];
 #pragma unroll
-    for (int i = 0; i < I_COUNT; ++i) iv[i] = ivp[i];
+    for (int i = 0; i < I_COUNT; ++i)
+      if (!cold_i(i)) iv[i] = ivp[i];
   }
   __device__ __forceinline__ void load_vectors() {
     ld(vp(V_Q), q);
@@ -267,9 +299,11 @@ struct NutsChain {
     double* sc = A.sc + (size_t)gid * S_COUNT;
     int* ivp = A.iv + (size_t)gid * I_COUNT;
 #pragma unroll
-    for (int i = 0; i < S_COUNT; ++i) sc[i] = s[i];
+    for (int i = 0; i < S_COUNT; ++i)
+      if (!cold_s(i)) sc[i] = s[i];
 #pragma unroll
-    for (int i = 0; i < I_COUNT; ++i) ivp[i] = iv[i];
+    for (int i = 0; i < I_COUNT; ++i)
+      if (!cold_i(i)) ivp[i] = iv[i];
     st(vp(V_Q), q);
     st(vp(V_P), p);
     st(vp(V_G), g);
@@ -295,8 +329,8 @@ struct NutsChain {
   // from the even one's call (u_key = the block's (iteration, m) + 1; 0 = nothing kept)
   uint64_t u_odd = 0, u_key = 0;
   __device__ __forceinline__ double uniform() {
-    const uint32_t it = (uint32_t)(iv[I_ITER] + A.iter_offset);
-    const uint32_t k = (uint32_t)iv[I_UK]++;
+    const uint32_t it = (uint32_t)(IV(I_ITER) + A.iter_offset);
+    const uint32_t k = (uint32_t)IV(I_UK)++;
     const uint64_t key = (((uint64_t)it << 32) | (k >> 1)) + 1;
     if ((k & 1) && key == u_key) return u53(u_odd);
     const u64x2 r = philox(A.seed, rid, it, k >> 1, TAG_UNI);
@@ -314,12 +348,12 @@ struct NutsChain {
   __device__ __forceinline__ void load_sample_point() {
     ld(vp(V_QS), q);
     ld(vp(V_GS), g);
-    s[S_V] = s[S_VS];
+    S(S_V) = S(S_VS);
   }
 
   // Request = the new q after begin_update_p + update_q (expl_leapfrog).
   __device__ __forceinline__ void begin_leapfrog(double eps) {
-    s[S_LFEPS] = eps;
+    S(S_LFEPS) = eps;
     const double he = 0.5 * eps;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
@@ -328,8 +362,8 @@ struct NutsChain {
     }
   }
   __device__ __forceinline__ void finish_leapfrog(double lp, const double (&glp)[NCH]) {
-    const double he = 0.5 * s[S_LFEPS];
-    s[S_V] = -lp;
+    const double he = 0.5 * S(S_LFEPS);
+    S(S_V) = -lp;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       g[k] = -glp[k];
@@ -339,28 +373,28 @@ struct NutsChain {
 
   // ---- init_stepsize (base_hmc) as a probe sequence, one leapfrog per step
   __device__ __forceinline__ bool start_probe() {
-    const double e = s[S_NOMEPS];
+    const double e = S(S_NOMEPS);
     if (e == 0 || e > 1e7 || isnan(e)) return false;
-    iv[I_PROBE] = 0;
-    iv[I_MODE] = M_PROBE;
+    IV(I_PROBE) = 0;
+    IV(I_MODE) = M_PROBE;
     load_sample_point();
-    sample_momentum((uint32_t)iv[I_SSCALL], 0u, TAG_SSMOM);
-    s[S_PH0] = s[S_V] + kinetic(p);
+    sample_momentum((uint32_t)IV(I_SSCALL), 0u, TAG_SSMOM);
+    S(S_PH0) = S(S_V) + kinetic(p);
     begin_leapfrog(e);
     return true;
   }
 
   // ---- adaptation (stepsize_adaptation, windowed var_adaptation)
   __device__ __forceinline__ void learn_stepsize(double adapt_stat) {
-    s[S_DA_CNT] += 1.0;
-    const DaState r = dual_averaging_cold(s[S_DA_CNT], s[S_SBAR], s[S_XBAR], s[S_MU], adapt_stat, A.t0, A.delta,
+    S(S_DA_CNT) += 1.0;
+    const DaState r = dual_averaging_cold(S(S_DA_CNT), S(S_SBAR), S(S_XBAR), S(S_MU), adapt_stat, A.t0, A.delta,
                                           A.gamma, A.kappa);
-    s[S_SBAR] = r.sbar;
-    s[S_XBAR] = r.xbar;
-    s[S_NOMEPS] = r.nomeps;
+    S(S_SBAR) = r.sbar;
+    S(S_XBAR) = r.xbar;
+    S(S_NOMEPS) = r.nomeps;
   }
   __device__ __forceinline__ bool learn_variance() {
-    const unsigned cnt = (unsigned)iv[I_WCNT];
+    const unsigned cnt = (unsigned)IV(I_WCNT);
     const unsigned nw = (unsigned)A.num_warmup;
     const bool in_window = (cnt >= A.init_buffer) && (cnt < nw - A.term_buffer) && (cnt != nw);
     double wm[NCH], wm2[NCH];
@@ -369,29 +403,29 @@ struct NutsChain {
     if (in_window) {
       double qs[NCH];
       ld(vp(V_QS), qs);
-      s[S_WFN] += 1.0;
+      S(S_WFN) += 1.0;
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
         const double delta = qs[k] - wm[k];
-        wm[k] += delta / s[S_WFN];
+        wm[k] += delta / S(S_WFN);
         wm2[k] += (qs[k] - wm[k]) * delta;
       }
     }
-    const bool end_window = (cnt == (unsigned)iv[I_WNEXT]) && (cnt != nw);
+    const bool end_window = (cnt == (unsigned)IV(I_WNEXT)) && (cnt != nw);
     if (end_window) {
       // compute_next_window
       const unsigned last = nw - A.term_buffer - 1;
-      if ((unsigned)iv[I_WNEXT] != last) {
-        unsigned size = (unsigned)iv[I_WSIZE] * 2;
+      if ((unsigned)IV(I_WNEXT) != last) {
+        unsigned size = (unsigned)IV(I_WSIZE) * 2;
         unsigned next = cnt + size;
         if (next != last) {
           const unsigned nb = next + 2 * size;
           if (nb >= nw - A.term_buffer) next = last;
         }
-        iv[I_WSIZE] = (int)size;
-        iv[I_WNEXT] = (int)next;
+        IV(I_WSIZE) = (int)size;
+        IV(I_WNEXT) = (int)next;
       }
-      const double n = s[S_WFN];
+      const double n = S(S_WFN);
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
         double v = im[k];
@@ -400,68 +434,68 @@ struct NutsChain {
         wm[k] = 0.0;
         wm2[k] = 0.0;
       }
-      s[S_WFN] = 0.0;
+      S(S_WFN) = 0.0;
       st(vp(V_IM), im);
     }
     st(vp(V_WM), wm);
     st(vp(V_WM2), wm2);
-    iv[I_WCNT] = (int)(cnt + 1);
+    IV(I_WCNT) = (int)(cnt + 1);
     return end_window;
   }
 
   // ---- transitions
   __device__ __forceinline__ void begin_subtree() {
-    iv[I_DIR] = uniform() > 0.5 ? 1 : -1;
-    const int f = iv[I_DIR] > 0;
+    IV(I_DIR) = uniform() > 0.5 ? 1 : -1;
+    const int f = IV(I_DIR) > 0;
     ld(vp(f ? V_QF : V_QB), q);
     ld(vp(f ? V_PF : V_PB), p);
     ld(vp(f ? V_GF : V_GB), g);
-    s[S_V] = f ? s[S_VF] : s[S_VB];
-    iv[I_LEAF] = 0;
-    begin_leapfrog(iv[I_DIR] * s[S_EPS]);
+    S(S_V) = f ? S(S_VF) : S(S_VB);
+    IV(I_LEAF) = 0;
+    begin_leapfrog(IV(I_DIR) * S(S_EPS));
   }
 
   __device__ __forceinline__ void start_transition() {
-    iv[I_MODE] = M_TRAJ;
-    s[S_EPS] = s[S_NOMEPS];   // base_hmc::sample_stepsize; jitter on its own stream (TAG_JIT)
+    IV(I_MODE) = M_TRAJ;
+    S(S_EPS) = S(S_NOMEPS);   // base_hmc::sample_stepsize; jitter on its own stream (TAG_JIT)
     if (A.jitter > 0)
-      s[S_EPS] *= 1.0 + A.jitter * (2.0 * uniform_at(A.seed, rid, (uint32_t)(iv[I_ITER] + A.iter_offset), 0u, TAG_JIT) - 1.0);
-    iv[I_UK] = 0;
+      S(S_EPS) *= 1.0 + A.jitter * (2.0 * uniform_at(A.seed, rid, (uint32_t)(IV(I_ITER) + A.iter_offset), 0u, TAG_JIT) - 1.0);
+    IV(I_UK) = 0;
     load_sample_point();
-    sample_momentum((uint32_t)(iv[I_ITER] + A.iter_offset), 0u, TAG_MOM);
-    const double H0 = s[S_V] + kinetic(p);
-    s[S_H0] = H0;
-    s[S_HS] = H0;
+    sample_momentum((uint32_t)(IV(I_ITER) + A.iter_offset), 0u, TAG_MOM);
+    const double H0 = S(S_V) + kinetic(p);
+    S(S_H0) = H0;
+    S(S_HS) = H0;
     st(vp(V_QF), q); st(vp(V_PF), p); st(vp(V_GF), g);
     st(vp(V_QB), q); st(vp(V_PB), p); st(vp(V_GB), g);
-    s[S_VF] = s[S_V];
-    s[S_VB] = s[S_V];
+    S(S_VF) = S(S_V);
+    S(S_VB) = S(S_V);
     double ps[NCH];
 #pragma unroll
     for (int k = 0; k < NCH; ++k) ps[k] = im[k] * p[k];
     st(vp(V_PSP), ps);
     st(vp(V_PSM), ps);
     st(vp(V_RHO), p);
-    s[S_LSW] = 0.0;
-    s[S_SUMMETRO] = 0.0;
-    iv[I_NLEAP] = 0;
-    iv[I_DEPTH] = 0;
-    iv[I_DIV] = 0;
+    S(S_LSW) = 0.0;
+    S(S_SUMMETRO) = 0.0;
+    IV(I_NLEAP) = 0;
+    IV(I_DEPTH) = 0;
+    IV(I_DIV) = 0;
     begin_subtree();
   }
 
   // After a transition (or its adaptation probes): stop, pause or go on.  Returns true
   // if a gradient request was issued.
   __device__ __forceinline__ bool continue_or_stop(int pause_at) {
-    if (iv[I_ITER] >= A.total_iters) { iv[I_MODE] = M_DONE; return false; }
-    if (iv[I_ITER] >= pause_at) { iv[I_MODE] = M_PAUSED; return false; }
+    if (IV(I_ITER) >= A.total_iters) { IV(I_MODE) = M_DONE; return false; }
+    if (IV(I_ITER) >= pause_at) { IV(I_MODE) = M_PAUSED; return false; }
     start_transition();
     return true;
   }
 
   __device__ __forceinline__ bool end_transition(int pause_at) {
-    const double accept = s[S_SUMMETRO] / (double)iv[I_NLEAP];
-    const int it = iv[I_ITER];
+    const double accept = S(S_SUMMETRO) / (double)IV(I_NLEAP);
+    const int it = IV(I_ITER);
     if (it >= A.ud_first) {
       double qs[NCH];
       ld(vp(V_QS), qs);
@@ -471,91 +505,91 @@ struct NutsChain {
       const int col = cidx * A.num_samples + (it - A.num_warmup);
       double qs[NCH];
       ld(vp(V_QS), qs);
-      write_draw<NCH, SEG>(A, sh, shard, col, qs, -s[S_VS], lane);
+      write_draw<NCH, SEG>(A, sh, shard, col, qs, -S(S_VS), lane);
       if (lane < N_STATS) {
         double v = 0;
         switch (lane) {
           case 0: v = accept; break;
-          case 1: v = s[S_EPS]; break;
-          case 2: v = (double)iv[I_DEPTH]; break;
-          case 3: v = (double)iv[I_NLEAP]; break;
-          case 4: v = (double)iv[I_DIV]; break;
-          default: v = s[S_HS]; break;
+          case 1: v = S(S_EPS); break;
+          case 2: v = (double)IV(I_DEPTH); break;
+          case 3: v = (double)IV(I_NLEAP); break;
+          case 4: v = (double)IV(I_DIV); break;
+          default: v = S(S_HS); break;
         }
         A.stats[((size_t)shard * A.S_total + col) * N_STATS + lane] = v;
       }
-      if (iv[I_DIV]) ++ndiv;
+      if (IV(I_DIV)) ++ndiv;
     }
     bool update = false;
     if (A.adapt && it < A.num_warmup) {
       learn_stepsize(accept);
       if (A.var_on) update = learn_variance();
     }
-    iv[I_ITER] = it + 1;
+    IV(I_ITER) = it + 1;
     if (update) {
-      iv[I_SSREASON] = (A.adapt && it + 1 == A.num_warmup) ? 2 : 1;
+      IV(I_SSREASON) = (A.adapt && it + 1 == A.num_warmup) ? 2 : 1;
       if (start_probe()) return true;
       finish_window_update();
     } else if (A.adapt && it + 1 == A.num_warmup) {
-      s[S_NOMEPS] = exp_cold(s[S_XBAR]);   // complete_adaptation
+      S(S_NOMEPS) = exp_cold(S(S_XBAR));   // complete_adaptation
     }
     return continue_or_stop(pause_at);
   }
 
   __device__ __forceinline__ void finish_window_update() {
-    s[S_MU] = log_cold(10.0 * s[S_NOMEPS]);
-    s[S_DA_CNT] = 0.0;
-    s[S_SBAR] = 0.0;
-    s[S_XBAR] = 0.0;
-    if (iv[I_SSREASON] == 2) s[S_NOMEPS] = exp_cold(s[S_XBAR]);
+    S(S_MU) = log_cold(10.0 * S(S_NOMEPS));
+    S(S_DA_CNT) = 0.0;
+    S(S_SBAR) = 0.0;
+    S(S_XBAR) = 0.0;
+    if (IV(I_SSREASON) == 2) S(S_NOMEPS) = exp_cold(S(S_XBAR));
   }
 
   __device__ __forceinline__ bool on_probe(double lp, const double (&glp)[NCH], int pause_at) {
     finish_leapfrog(lp, glp);
-    double h = s[S_V] + kinetic(p);
+    double h = S(S_V) + kinetic(p);
     if (isnan(h)) h = INFINITY;
-    const double dH = s[S_PH0] - h;
+    const double dH = S(S_PH0) - h;
     const double l08 = log(0.8);
     bool more = true;
-    if (iv[I_PROBE] == 0) {
-      iv[I_PDIR] = dH > l08 ? 1 : -1;
-    } else if ((iv[I_PDIR] == 1 && !(dH > l08)) || (iv[I_PDIR] == -1 && !(dH < l08))) {
+    if (IV(I_PROBE) == 0) {
+      IV(I_PDIR) = dH > l08 ? 1 : -1;
+    } else if ((IV(I_PDIR) == 1 && !(dH > l08)) || (IV(I_PDIR) == -1 && !(dH < l08))) {
       more = false;
     } else {
-      s[S_NOMEPS] = iv[I_PDIR] == 1 ? 2 * s[S_NOMEPS] : 0.5 * s[S_NOMEPS];
-      if (s[S_NOMEPS] > 1e7 || s[S_NOMEPS] == 0) {
-        iv[I_MODE] = M_ERROR;
+      S(S_NOMEPS) = IV(I_PDIR) == 1 ? 2 * S(S_NOMEPS) : 0.5 * S(S_NOMEPS);
+      if (S(S_NOMEPS) > 1e7 || S(S_NOMEPS) == 0) {
+        IV(I_MODE) = M_ERROR;
         load_sample_point();
         return false;
       }
     }
     if (more) {
-      iv[I_PROBE] += 1;
+      IV(I_PROBE) += 1;
       load_sample_point();
-      sample_momentum((uint32_t)iv[I_SSCALL], (uint32_t)iv[I_PROBE] << 12, TAG_SSMOM);
-      s[S_PH0] = s[S_V] + kinetic(p);
-      begin_leapfrog(s[S_NOMEPS]);
+      sample_momentum((uint32_t)IV(I_SSCALL), (uint32_t)IV(I_PROBE) << 12, TAG_SSMOM);
+      S(S_PH0) = S(S_V) + kinetic(p);
+      begin_leapfrog(S(S_NOMEPS));
       return true;
     }
-    iv[I_SSCALL] += 1;
+    IV(I_SSCALL) += 1;
     load_sample_point();
-    if (iv[I_SSREASON] >= 1) finish_window_update();
+    if (IV(I_SSREASON) >= 1) finish_window_update();
     return continue_or_stop(pause_at);
   }
 
   __device__ __forceinline__ bool on_leaf(double lp, const double (&glp)[NCH], int pause_at) {
     finish_leapfrog(lp, glp);
     ++nleap;
-    const double H0 = s[S_H0];
-    double h = s[S_V] + kinetic(p);
+    const double H0 = S(S_H0);
+    double h = S(S_V) + kinetic(p);
     if (isnan(h)) h = INFINITY;
-    if ((h - H0) > 1000.0) iv[I_DIV] = 1;
-    iv[I_NLEAP] += 1;
-    s[S_SUMMETRO] += (H0 - h > 0) ? 1.0 : exp(H0 - h);
+    if ((h - H0) > 1000.0) IV(I_DIV) = 1;
+    IV(I_NLEAP) += 1;
+    S(S_SUMMETRO) += (H0 - h > 0) ? 1.0 : exp(H0 - h);
     // the leaf as a depth-0 sub-tree
     double c_lsw = H0 - h;
     double c_rho[NCH], c_psb[NCH], c_pse[NCH], c_q[NCH], c_g[NCH], c_pb[NCH];
-    double c_V = s[S_V], c_H = h;
+    double c_V = S(S_V), c_H = h;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       c_rho[k] = p[k];
@@ -565,9 +599,9 @@ struct NutsChain {
       c_g[k] = g[k];
       c_pb[k] = p[k];
     }
-    if (iv[I_DIV]) return end_transition(pause_at);
-    const int depth = iv[I_DEPTH];
-    const int n = iv[I_LEAF];
+    if (IV(I_DIV)) return end_transition(pause_at);
+    const int depth = IV(I_DEPTH);
+    const int n = IV(I_LEAF);
     int j = 0;
     while (j < depth && ((n >> j) & 1)) {
       // merge pending left sub-tree (level j) with the just-completed right one
@@ -626,12 +660,12 @@ struct NutsChain {
       stks[j * SS_COUNT + SS_LSW] = c_lsw;
       stks[j * SS_COUNT + SS_V] = c_V;
       stks[j * SS_COUNT + SS_H] = c_H;
-      iv[I_LEAF] = n + 1;
-      begin_leapfrog(iv[I_DIR] * s[S_EPS]);
+      IV(I_LEAF) = n + 1;
+      begin_leapfrog(IV(I_DIR) * S(S_EPS));
       return true;
     }
     // the top-level sub-tree of this depth is complete and valid
-    const int fwd = iv[I_DIR] > 0;
+    const int fwd = IV(I_DIR) > 0;
     double o_p[NCH], o_ps[NCH];     // the old trajectory's end next to the new sub-tree
     if (A.uturn_ext) {
       ld(vp(fwd ? V_PF : V_PB), o_p);
@@ -640,17 +674,17 @@ struct NutsChain {
     st(vp(fwd ? V_QF : V_QB), q);
     st(vp(fwd ? V_PF : V_PB), p);
     st(vp(fwd ? V_GF : V_GB), g);
-    if (fwd) s[S_VF] = s[S_V];            // (no run-time index into the register arrays: that
-    else s[S_VB] = s[S_V];                //  would move them to scratch)
-    iv[I_DEPTH] = depth + 1;
+    if (fwd) S(S_VF) = S(S_V);            // (no run-time index into the register arrays: that
+    else S(S_VB) = S(S_V);                //  would move them to scratch)
+    IV(I_DEPTH) = depth + 1;
     const double u = uniform();
-    if (c_lsw > s[S_LSW] || u < exp(c_lsw - s[S_LSW])) {
+    if (c_lsw > S(S_LSW) || u < exp(c_lsw - S(S_LSW))) {
       st(vp(V_QS), c_q);
       st(vp(V_GS), c_g);
-      s[S_VS] = c_V;
-      s[S_HS] = c_H;
+      S(S_VS) = c_V;
+      S(S_HS) = c_H;
     }
-    s[S_LSW] = log_sum_exp2(s[S_LSW], c_lsw);
+    S(S_LSW) = log_sum_exp2(S(S_LSW), c_lsw);
     double rho[NCH], psp[NCH], psm[NCH], rho_old[NCH];
     ld(vp(V_RHO), rho);
 #pragma unroll
@@ -684,22 +718,22 @@ struct NutsChain {
       junction_ok = ok2 && ok3;
     }
     if (!junction_ok) return end_transition(pause_at);
-    if (!criterion(psm, psp, rho) || iv[I_DEPTH] >= A.max_depth) return end_transition(pause_at);
+    if (!criterion(psm, psp, rho) || IV(I_DEPTH) >= A.max_depth) return end_transition(pause_at);
     begin_subtree();
     return true;
   }
 
   // Consume the evaluation requested last step.  Returns true if a new request (at q) was issued.
   __device__ __forceinline__ bool consume(double lp, const double (&glp)[NCH], int pause_at) {
-    switch (iv[I_MODE]) {
+    switch (IV(I_MODE)) {
       case M_INIT: {
-        s[S_V] = -lp;
+        S(S_V) = -lp;
 #pragma unroll
         for (int k = 0; k < NCH; ++k) g[k] = -glp[k];
         st(vp(V_QS), q);
         st(vp(V_GS), g);
-        s[S_VS] = s[S_V];
-        iv[I_SSREASON] = 0;
+        S(S_VS) = S(S_V);
+        IV(I_SSREASON) = 0;
         if (!A.skip_ss && start_probe()) return true;
         return continue_or_stop(pause_at);
       }
@@ -710,7 +744,7 @@ struct NutsChain {
   }
 
   __device__ __forceinline__ bool resume(int pause_at) {   // PAUSED -> next transition
-    if (iv[I_MODE] != M_PAUSED) return false;
+    if (IV(I_MODE) != M_PAUSED) return false;
     return continue_or_stop(pause_at);
   }
 };
@@ -760,11 +794,11 @@ __global__ __launch_bounds__(64) void k_nuts_step(NutsArgs A, int step_id, int p
   const int gid = blockIdx.x, lane = threadIdx.x;
   NutsChain<NCH> ch(A, gid, lane);
   ch.load();
-  const int mode = ch.iv[I_MODE];
+  const int mode = ch.IV(I_MODE);
   if (mode == M_DONE || mode == M_ERROR) return;
   bool req;
   if (mode == M_PAUSED) {
-    if (ch.iv[I_ITER] >= pause_at) return;
+    if (ch.IV(I_ITER) >= pause_at) return;
     req = ch.resume(pause_at);
   } else {
     double glp[NCH];
@@ -797,7 +831,10 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   extern __shared__ double fl_all[];
   const size_t nv = (size_t)V_COUNT * A.Dp, ns = (size_t)A.max_depth * stack_vecs(A) * A.Dp;
   const size_t nss = (size_t)A.max_depth * SS_COUNT;
-  double* const fl = fl_all + (size_t)seg * (nv + ns + nss);
+  constexpr size_t nsc = S_COUNT + (I_COUNT + 1) / 2;   // the chain's scalars and counters
+  double* const fl = fl_all + (size_t)seg * (nv + ns + nss + nsc);
+  double* const lsc = fl + nv + ns + nss;
+  int* const liv = (int*)(lsc + S_COUNT);
   double* const gvec = A.vec + (size_t)gid * nv;
   double* const gstk = A.stk + (size_t)gid * A.max_depth * SV_COUNT * A.Dp;   // (allocation stride; ns used)
   double* const gstks = A.stks + (size_t)gid * nss;
@@ -810,17 +847,19 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
     for (size_t i = lane; i < nv; i += SEG) fl[i] = gvec[i];
     for (size_t i = lane; i < ns; i += SEG) fl[nv + i] = gstk[i];
     for (size_t i = lane; i < nss; i += SEG) fl[nv + ns + i] = gstks[i];
+    for (int i = lane; i < S_COUNT; i += SEG) lsc[i] = A.sc[(size_t)gid * S_COUNT + i];
+    for (int i = lane; i < I_COUNT; i += SEG) liv[i] = A.iv[(size_t)gid * I_COUNT + i];
   }
   __syncthreads();
   if (run) {
-    NutsChain<NCH, SEG> ch(A, gid, lane, fl, fl + nv, fl + nv + ns);
+    NutsChain<NCH, SEG> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
     ch.load();
     double yc[NCH], sc[NCH];
     schools_data<NCH, SEG>(ch.sh, yc, sc, lane, ch.D);
-    const int mode = ch.iv[I_MODE];
+    const int mode = ch.IV(I_MODE);
     bool req = false, go = true;
     if (mode == M_PAUSED) {
-      if (ch.iv[I_ITER] >= pause_at) {
+      if (ch.IV(I_ITER) >= pause_at) {
         go = false;
       } else {
         req = ch.resume(pause_at);
@@ -853,6 +892,10 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
     for (size_t i = lane; i < nv; i += SEG) gvec[i] = fl[i];
     for (size_t i = lane; i < ns; i += SEG) gstk[i] = fl[nv + i];
     for (size_t i = lane; i < nss; i += SEG) gstks[i] = fl[nv + ns + i];
+    for (int i = lane; i < S_COUNT; i += SEG)
+      if (NutsChain<NCH, SEG>::cold_s(i)) A.sc[(size_t)gid * S_COUNT + i] = lsc[i];
+    for (int i = lane; i < I_COUNT; i += SEG)
+      if (NutsChain<NCH, SEG>::cold_i(i)) A.iv[(size_t)gid * I_COUNT + i] = liv[i];
   }
 }
 
@@ -892,7 +935,7 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
 template <int NCH, int CPW, int MINW = 1>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
   const size_t lds = CPW * sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp +
-                                             (size_t)A.max_depth * SS_COUNT);
+                                             (size_t)A.max_depth * SS_COUNT + S_COUNT + (I_COUNT + 1) / 2);
   if (lds > 64 * 1024) {
     // the attribute is per device (allow_big_lds keys it on the current one); a failure is
     // reported as such rather than as a generic launch failure

@@ -461,12 +461,13 @@ constexpr int S3_MAXP = 7;        // pieces per lane in the forward: K <= 56
 constexpr int S3_KMAX = 52;       // pieces per row (d/2) handled by v3
 
 
-// DPP lane exchange of a double (full-rate VALU, no LDS round trip like ds_bpermute).
+// DPP lane exchange of a double (full-rate VALU, no LDS round trip like ds_bpermute); bound_ctrl
+// zero-fills as old = 0 would, without a v_mov of the old value before each move.
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
   const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, true);
   return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 // Sum over each group of 8 consecutive lanes; every lane of the group gets the total:
