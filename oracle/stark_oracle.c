@@ -185,15 +185,19 @@ int orc_dim(const orc_data* m) {
 
 /* 8 schools, example/schools.stan:1-18, unconstrained q = (mu, log tau, eta[1..J]).
  * eta ~ normal(0,1) (schools.stan:15), y ~ normal(theta, sigma) (:16), theta = mu + tau*eta
- * (:11-12), tau = exp(u) with log-Jacobian u (real<lower=0> tau, :7); flat mu, tau. */
+ * (:11-12), tau = exp(u) with log-Jacobian u (real<lower=0> tau, :7); flat mu, tau.
+ * normal_lpdf's arithmetic as Stan Math 2.18/2.19 (the release pystan 2.19 ships; third-party,
+ * not in the reference) does it: inv_sigma = 1 / sigma, z = (y - theta) * inv_sigma, the
+ * partial wrt theta inv_sigma * z. */
 double orc_schools_lpgrad(int J, const double* y, const double* sigma, const double* q, double* grad) {
   double mu = q[0], u = q[1], tau = exp(u);
   double lp = 0.0, smu = 0.0, su = 0.0;
   for (int j = 0; j < J; ++j) {
     double eta = q[2 + j];
     double theta = mu + tau * eta;
-    double z = (y[j] - theta) / sigma[j];
-    double r = z / sigma[j];
+    double inv_sigma = 1.0 / sigma[j];
+    double z = (y[j] - theta) * inv_sigma;
+    double r = inv_sigma * z;
     lp += -0.5 * eta * eta - 0.5 * z * z;
     smu += r;
     su += r * eta;

@@ -101,21 +101,23 @@ __device__ __forceinline__ double log_sum_exp2(double a, double b) {   // stan::
 // ------------------------------------------------------------------ model hooks
 // 8 schools (example/schools.stan:1-18): q = (mu, log tau, eta_1..J); returns lp, writes
 // grad lp.  Mirrors oracle orc_schools_lpgrad.
-// y_j and sigma_j of this lane's schools (element e = k SEG + lane is school e - 2), loaded once
-// per launch instead of two global loads per leapfrog (their latency was on every leapfrog's
-// critical path at one wave per SIMD)
+// y_j and 1 / sigma_j of this lane's schools (element e = k SEG + lane is school e - 2), loaded
+// once per launch instead of two global loads per leapfrog (their latency was on every
+// leapfrog's critical path at one wave per SIMD).  normal_lpdf as Stan Math 2.18/2.19 computes
+// it: inv_sigma = 1 / sigma once, then (y - theta) * inv_sigma and the partial inv_sigma * z --
+// no division per leapfrog (oracle orc_schools_lpgrad does the same arithmetic).
 template <int NCH, int SEG = WAVE>
-__device__ __forceinline__ void schools_data(const ShardDev& sh, double (&yc)[NCH], double (&sc)[NCH], int lane, int D) {
+__device__ __forceinline__ void schools_data(const ShardDev& sh, double (&yc)[NCH], double (&isc)[NCH], int lane, int D) {
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int e = k * SEG + lane;
     const bool in = e >= 2 && e < D;
     yc[k] = in ? sh.y[e - 2] : 0.0;
-    sc[k] = in ? sh.sigma[e - 2] : 1.0;
+    isc[k] = in ? 1.0 / sh.sigma[e - 2] : 1.0;
   }
 }
 template <int NCH, int SEG = WAVE>
-__device__ double schools_lpgrad(const double (&yc)[NCH], const double (&sc)[NCH], const double (&q)[NCH],
+__device__ double schools_lpgrad(const double (&yc)[NCH], const double (&isc)[NCH], const double (&q)[NCH],
                                  double (&glp)[NCH], int lane, int D) {
   const double mu = seg_bcast<SEG, 0>(q[0]);
   const double u = seg_bcast<SEG, 1>(q[0]);
@@ -128,9 +130,8 @@ __device__ double schools_lpgrad(const double (&yc)[NCH], const double (&sc)[NCH
     if (e >= 2 && e < D) {
       const double eta = q[k];
       const double theta = mu + tau * eta;
-      const double sj = sc[k];
-      const double z = (yc[k] - theta) / sj;
-      const double r = z / sj;
+      const double z = (yc[k] - theta) * isc[k];
+      const double r = isc[k] * z;
       lp += -0.5 * eta * eta - 0.5 * z * z;
       smu += r;
       su += r * eta;
@@ -854,8 +855,8 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   if (run) {
     NutsChain<NCH, SEG> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
     ch.load();
-    double yc[NCH], sc[NCH];
-    schools_data<NCH, SEG>(ch.sh, yc, sc, lane, ch.D);
+    double yc[NCH], isc[NCH];
+    schools_data<NCH, SEG>(ch.sh, yc, isc, lane, ch.D);
     const int mode = ch.IV(I_MODE);
     bool req = false, go = true;
     if (mode == M_PAUSED) {
@@ -874,7 +875,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
       unsigned long long ngrad = 0;
       while (req && steps < max_steps) {
         double glp[NCH];
-        const double lp = schools_lpgrad<NCH, SEG>(yc, sc, ch.q, glp, lane, ch.D);
+        const double lp = schools_lpgrad<NCH, SEG>(yc, isc, ch.q, glp, lane, ch.D);
         ++steps;
         req = ch.consume(lp, glp, pause_at);
         if (req) ++ngrad;
@@ -911,9 +912,9 @@ __global__ __launch_bounds__(64) void k_schools_lpgrad(const ShardDev* shards, i
     const int e = k * WAVE + lane;
     qq[k] = e < sh.D ? q[(size_t)c * Dp + e] : 0.0;
   }
-  double yc[NCH], sc[NCH];
-  schools_data<NCH>(sh, yc, sc, lane, sh.D);
-  const double v = schools_lpgrad<NCH>(yc, sc, qq, gl, lane, sh.D);
+  double yc[NCH], isc[NCH];
+  schools_data<NCH>(sh, yc, isc, lane, sh.D);
+  const double v = schools_lpgrad<NCH>(yc, isc, qq, gl, lane, sh.D);
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int e = k * WAVE + lane;
