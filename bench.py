@@ -460,10 +460,10 @@ def main():
                         "the full-data posterior (MAP + inverse Hessian of the GPU gradient, tools/laplace.py)")
 
     # ---- roofline of the dominant kernel (the data sweep)
-    # C = 16: k_sweepm, X.[beta_1..beta_16] on fp64 MFMA, bound by the fp64 pipe;
+    # C = 16: k_sweepe (d = 50, 100) or k_sweepm, X.[beta_1..beta_16] on fp64 MFMA;
     # C <= 4: k_sweep3 (VALU), bound by HBM.
     mfma = a.chains == 16
-    kname = ("k_sweepe" if a.d == 100 else "k_sweepm") if mfma else "k_sweep3"
+    kname = ("k_sweepe" if a.d in (50, 100) else "k_sweepm") if mfma else "k_sweep3"
     ybytes = 4 if a.family == "logistic" else 8
     fam = "LOGREG" if a.family == "logistic" else "LINREG"
     bytes_per_shard = rows_per_shard * (8 * a.d + ybytes)   # X fp64 + y (int32 / fp64), once per sweep
