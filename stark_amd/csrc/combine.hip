@@ -28,6 +28,7 @@
 #include "common.h"
 #include <math.h>
 #include <algorithm>
+#include <utility>
 
 namespace stk {
 
@@ -265,27 +266,50 @@ __global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t*
 // the folded terms do not cancel).  Shard b with used[b] == 0 (NaN draws) gets W = 0 and no
 // status; status[b] = 1 when a pivot is <= 64 P eps or NaN (a singular covariance; numpy's inv
 // raises LinAlgError only on an exactly zero LU pivot and otherwise returns rounding noise).
+// Row k of the tile (rk) sits in lane (k, g) of every 16-lane row: a DPP row_newbcast:k move per
+// register, no LDS crossbar; the pivot a[k][k] is one lane's, read as a scalar; only column k
+// (c, lane (r, k mod 4) of another row) still needs a ds_bpermute -- one per pivot instead of six.
+template <int CTRL>
+__device__ __forceinline__ double cb_dpp(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int L>
+__device__ __forceinline__ double cb_lane(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)b, L);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), L);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <int K>
+__device__ __forceinline__ void inv16_pivot(double (&a)[4], int lr, int lg, double pmin, int& sing) {
+  constexpr int kg = K & 3, ks = K >> 2;
+  const double c = __shfl(a[ks], lr + 16 * kg);          // a[r][k]
+  double rk[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) rk[s] = cb_dpp<0x150 + K>(a[s]);   // a[k][g + 4s]
+  const double piv = cb_lane<K + 16 * kg>(a[ks]);         // a[k][k], wave-uniform
+  if (!(piv > pmin)) sing = 1;
+  double ip = __builtin_amdgcn_rcp(piv);
+  ip = fma(ip, fma(-piv, ip, 1.0), ip);
+  ip = fma(ip, fma(-piv, ip, 1.0), ip);
+  const double cc = (lr == K) ? c - 1.0 : c;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const double rj = (lg + 4 * s == K) ? 1.0 + ip : rk[s] * ip;
+    a[s] = fma(-cc, rj, a[s]);
+  }
+}
+template <int... K>
+__device__ __forceinline__ void inv16_all(double (&a)[4], int lr, int lg, double pmin, int& sing,
+                                          std::integer_sequence<int, K...>) {
+  (inv16_pivot<K>(a, lr, lg, pmin, sing), ...);
+}
 __device__ __forceinline__ int inv16(double (&a)[4], int lr, int lg, double pmin) {
   int sing = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int kg = k & 3, ks = k >> 2;
-    const double c = __shfl(a[ks], lr + 16 * kg);          // a[r][k]
-    double rk[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) rk[s] = __shfl(a[s], k + 16 * lg);   // a[k][g + 4s]
-    const double piv = __shfl(a[ks], k + 16 * kg);         // a[k][k], wave-uniform
-    if (!(piv > pmin)) sing = 1;
-    double ip = __builtin_amdgcn_rcp(piv);
-    ip = fma(ip, fma(-piv, ip, 1.0), ip);
-    ip = fma(ip, fma(-piv, ip, 1.0), ip);
-    const double cc = (lr == k) ? c - 1.0 : c;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const double rj = (lg + 4 * s == k) ? 1.0 + ip : rk[s] * ip;
-      a[s] = fma(-cc, rj, a[s]);
-    }
-  }
+  inv16_all(a, lr, lg, pmin, sing, std::make_integer_sequence<int, 16>{});
   return sing;
 }
 
