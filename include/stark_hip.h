@@ -205,7 +205,7 @@ STK_API int stk_transition(stk_model* m, int shard, double* q, int32_t C, uint64
  * left out because of NaN draws.  Singular matrices (STK_E_LINALG, numpy's LinAlgError):
  *   - stk_consensus / _blocked / _products invert each sample covariance and sum W, which are
  *     symmetric positive (semi)definite by construction, by diagonal-pivot block Gauss-Jordan on
- *     the unit-diagonal matrix and report a pivot <= 64 P eps or NaN as singular.  S <= p draws
+ *     the unit-diagonal matrix and report a pivot <= P eps or NaN as singular.  S <= p draws
  *     (p = P, or the largest row_block block) give a rank-deficient covariance (rank <= S - 1)
  *     and raise before any arithmetic; np.linalg.inv's LU usually returns a huge finite
  *     "inverse" built from rounding noise there, and raises only on an exactly zero pivot (a

@@ -31,6 +31,7 @@ SweepWs stk_sweep_ws(void* base, int64_t n_max, int d, int nshards);
 hipError_t stk_launch_sweep_reduce(int family, const ShardDev* shards_dev, int shard0, int nsh, int d, int G, int Gs,
                                    const double* q, int C, int Dp, double* partial, const int* req_step, int step_id,
                                    double* lp_out, double* g_out, hipStream_t st);
+hipError_t stk_launch_check_y01(const int32_t* y, int64_t n, int64_t* first, hipStream_t st);
 hipError_t stk_launch_gen_shard(double* X, double* yd, int32_t* yi, int64_t nrows, int d, int64_t grow0,
                                 uint64_t seed, double alpha, const double* beta, double noise_sigma, int family,
                                 hipStream_t st);
@@ -297,24 +298,31 @@ int stk_model_create(stk_ctx* ctx, int family, const stk_shard* shards, int nsha
       sd.x = (const double*)p;
       if (family == STK_LOGREG) {
         if (!in.y_int) { stk_set_error("shard %d: logreg needs y_int", s); rc = STK_E_ARG; break; }
-        {   // bernoulli_logit: y in {0, 1} (the sweeps read y as a sign bit)
-          std::vector<int32_t> yh(in.n_rows);
-          if (hipMemcpy(yh.data(), in.y_int, sizeof(int32_t) * in.n_rows, hipMemcpyDefault) != hipSuccess) {
-            stk_set_error("shard %d: y_int is not readable", s);
-            rc = STK_E_ARG;
+        if ((rc = upload(m, in.y_int, sizeof(int32_t) * in.n_rows, &p))) break;
+        sd.yi = (const int32_t*)p;
+        {   // bernoulli_logit: y in {0, 1} (the sweeps read y as a sign bit), checked on the device
+            // copy by a reduction that returns the first bad row (8 bytes back, not the shard)
+          DevBuf flag;
+          if ((rc = flag.ensure(sizeof(int64_t)))) break;
+          int64_t bad = -1;
+          int32_t v = 0;
+          hipError_t e = stk_launch_check_y01(sd.yi, in.n_rows, flag.as<int64_t>(), m->ctx->stream);
+          if (e == hipSuccess) e = hipMemcpyAsync(&bad, flag.p, sizeof(int64_t), hipMemcpyDeviceToHost, m->ctx->stream);
+          if (e == hipSuccess) e = hipStreamSynchronize(m->ctx->stream);
+          if (e == hipSuccess && bad >= 0 && bad < in.n_rows)
+            e = hipMemcpy(&v, sd.yi + bad, sizeof(int32_t), hipMemcpyDeviceToHost);
+          flag.release();
+          if (e != hipSuccess) {
+            stk_set_error("shard %d: y_int check failed: %s", s, hipGetErrorString(e));
+            rc = STK_E_HIP;
             break;
           }
-          int64_t bad = -1;
-          for (int64_t i = 0; i < in.n_rows && bad < 0; ++i)
-            if (yh[i] != 0 && yh[i] != 1) bad = i;
-          if (bad >= 0) {
-            stk_set_error("shard %d: y_int[%lld] = %d; bernoulli_logit needs 0 or 1", s, (long long)bad, yh[bad]);
+          if (bad >= 0 && bad < in.n_rows) {
+            stk_set_error("shard %d: y_int[%lld] = %d; bernoulli_logit needs 0 or 1", s, (long long)bad, v);
             rc = STK_E_ARG;
             break;
           }
         }
-        if ((rc = upload(m, in.y_int, sizeof(int32_t) * in.n_rows, &p))) break;
-        sd.yi = (const int32_t*)p;
       } else {
         if (!in.y) { stk_set_error("shard %d: linreg needs y", s); rc = STK_E_ARG; break; }
         if ((rc = upload(m, in.y, sizeof(double) * in.n_rows, &p))) break;
@@ -1044,15 +1052,18 @@ int combine_check(const std::vector<int32_t>& h, int nshards, int32_t* shard_use
   }
   return STK_OK;
 }
-// device memory (hipMalloc / a torch cuda tensor): the combine reads the draws and writes the
-// result in place instead of staging them through the context's scratch buffers
-bool is_device_ptr(const void* p) {
+// device memory ON THE CONTEXT'S DEVICE (hipMalloc / a torch cuda tensor): the combine reads the
+// draws and writes the result in place instead of staging them through the context's scratch
+// buffers.  Memory of another device is not used in place (the kernels would dereference it
+// without peer access): it takes the staged hipMemcpyAsync(Default) path, which copies across
+// devices.
+bool is_device_ptr(const void* p, int device) {
   hipPointerAttribute_t a{};
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
-  return a.type == hipMemoryTypeDevice;
+  return a.type == hipMemoryTypeDevice && a.device == device;
 }
 int consensus_run(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P, int32_t S, const int32_t* row_block,
                   double* sum_w, double* sum_wtheta, double* out, int32_t* shard_used) {
@@ -1082,7 +1093,7 @@ int consensus_run(stk_ctx* ctx, const double* draws, int32_t nshards, int32_t P,
   }
   CombineBufs b;
   RC(combine_bufs(ctx, nshards, P, S, &b));
-  const bool dev_in = is_device_ptr(draws), dev_out = out && is_device_ptr(out);
+  const bool dev_in = is_device_ptr(draws, ctx->device), dev_out = out && is_device_ptr(out, ctx->device);
   const double* X = dev_in ? draws : b.X;
   if (!dev_in) STK_HIP_CHECK(hipMemcpyAsync(b.X, draws, sizeof(double) * per * nshards, hipMemcpyDefault, st));
   if (row_block) STK_HIP_CHECK(hipMemcpyAsync(b.blk, row_block, sizeof(int32_t) * P, hipMemcpyDefault, st));

@@ -15,7 +15,7 @@
 //   k_spd_inverse    W_s = inv(cov_s): block Gauss-Jordan on 16 x 16 tiles held in registers,
 //                    fp64 MFMA updates (P <= 128), diagonal pivots -- a covariance is
 //                    symmetric positive (semi)definite, where diagonal pivoting is stable
-//                    (Cholesky's argument); a pivot <= 64 P eps or NaN is reported as singular
+//                    (Cholesky's argument); a pivot <= P eps or NaN is reported as singular
 //                    (LinAlgError).  One workgroup per shard, shards in parallel.  P > 128
 //                    falls back to k_gj_inverse (partial pivoting, global memory).
 //   k_sum_w          sum_s W_s in shard order (NaN shards hold W = 0)
@@ -264,7 +264,7 @@ __global__ void k_shard_used(const int32_t* rowbad, int P, int nshards, int32_t*
 // k with cross-lane shuffles and does the folded rank-1 step a_ij -= c_i r_j (c_k = a_kk - 1,
 // r_k = 1 + 1/a_kk, r_j = a_kj / a_kk: Gauss-Jordan with no per-element cases; with pivots <= 1
 // the folded terms do not cancel).  Shard b with used[b] == 0 (NaN draws) gets W = 0 and no
-// status; status[b] = 1 when a pivot is <= 64 P eps or NaN (a singular covariance; numpy's inv
+// status; status[b] = 1 when a pivot is <= P eps or NaN (a singular covariance; numpy's inv
 // raises LinAlgError only on an exactly zero LU pivot and otherwise returns rounding noise).
 // Row k of the tile (rk) sits in lane (k, g) of every 16-lane row: a DPP row_newbcast:k move per
 // register, no LDS crossbar; the pivot a[k][k] is one lane's, read as a scalar; only column k
@@ -329,8 +329,10 @@ __global__ __launch_bounds__(512) void k_spd_inverse(const double* Min, double* 
     return;
   }
   // pivots of the unit-diagonal matrix lie in (0, 1]; one at the rounding level of the
-  // elimination (<= 64 P eps) means a numerically singular covariance, reported as singular
-  const double pmin = 64.0 * P * 2.220446049250313e-16;
+  // elimination (<= P eps) means a numerically singular covariance (linearly dependent rows),
+  // reported as singular.  A full-rank but strongly correlated covariance (1 - R^2 ~ 1e-12,
+  // condition number ~1e12) stays above it and is inverted, as numpy's inv does
+  const double pmin = P * 2.220446049250313e-16;
   int sing = 0;
   if (tid < 128) {
     const double dii = tid < P ? M[(size_t)tid * P + tid] : 1.0;

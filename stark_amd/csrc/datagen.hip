@@ -58,9 +58,42 @@ __global__ __launch_bounds__(256) void k_gen_shard(double* X, double* yd, int32_
   }
 }
 
+// y in {0, 1} check of a bernoulli_logit shard (stk_model_create): *first = the first row whose
+// y is neither, or INT64_MAX.  Each block takes the minimum over its rows, one atomicMin per block.
+__global__ __launch_bounds__(256) void k_check_y01(const int32_t* y, int64_t n, unsigned long long* first) {
+  __shared__ unsigned long long m[4];
+  unsigned long long b = ~0ull >> 1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int32_t v = y[i];
+    if ((v != 0 && v != 1) && (unsigned long long)i < b) b = (unsigned long long)i;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long t = __shfl_xor(b, o);
+    b = t < b ? t : b;
+  }
+  if ((threadIdx.x & 63) == 0) m[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) b = m[w] < b ? m[w] : b;
+    if (b != (~0ull >> 1)) atomicMin(first, b);
+  }
+}
+
+__global__ void k_set_i64(int64_t* p, int64_t v) { *p = v; }
+
 }  // namespace stk
 
 using namespace stk;
+
+hipError_t stk_launch_check_y01(const int32_t* y, int64_t n, int64_t* first, hipStream_t st) {
+  hipLaunchKernelGGL(k_set_i64, dim3(1), dim3(1), 0, st, first, (int64_t)(~0ull >> 1));
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_check_y01, dim3((unsigned)blocks), dim3(256), 0, st, y, n,
+                     reinterpret_cast<unsigned long long*>(first));
+  return hipGetLastError();
+}
 
 hipError_t stk_launch_gen_shard(double* X, double* yd, int32_t* yi, int64_t nrows, int d, int64_t grow0,
                                 uint64_t seed, double alpha, const double* beta, double noise_sigma, int family,

@@ -464,6 +464,9 @@ def consensus(draws, ctx: Context | None = None, separate_lp: bool = False):
     if dev is not None:
         import torch
         ns, P, S = (int(v) for v in dev.shape)
+        if dev.device.index != ctx.device:
+            raise ValueError(f"draws on {dev.device} but the context is on cuda:{ctx.device}: pass a context "
+                             f"of the draws' device (engine.Context({dev.device.index}))")
         out_t = torch.empty((P, S), dtype=torch.float64, device=dev.device)
         used = np.empty(ns, np.int32)
         torch.cuda.current_stream(dev.device).synchronize()    # the library runs on its own stream

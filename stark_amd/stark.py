@@ -149,7 +149,12 @@ def sampling_config(family, datas, **kw):
         cfg["init"] = np.concatenate([_unconstrain(family, d, init[c]) for d in datas for c in range(chains)])
     elif init != "random":
         raise ValueError(f"unsupported init {init!r}")
-    for k in ("verbose", "refresh", "sample_file", "diagnostic_file", "check_hmc_diagnostics", "algorithm"):
+    for k in ("sample_file", "diagnostic_file"):
+        # pystan writes Stan CSV files here; this build returns draws only, so a caller who asks
+        # for a file is told, not silently handed none
+        if kw.pop(k, None) is not None:
+            raise NotImplementedError(f"{k}= (pystan's CSV output) is not supported: the draws are returned in memory")
+    for k in ("verbose", "refresh", "check_hmc_diagnostics", "algorithm"):
         v = kw.pop(k, None)
         if k == "algorithm" and v not in (None, "NUTS"):
             raise NotImplementedError("only algorithm='NUTS' is supported")
@@ -244,7 +249,13 @@ class Stark:
         cross-covariances turn that offset into an error of the parameter means (mean z^2 of
         4-7 at N = 1e8).  For accuracy pass separate_lp=True: lp__ gets a
         1 x 1 weight block of its own and the parameters are combined from their own
-        covariance (engine.consensus).  permuted=False keeps chain order in the draws."""
+        covariance (engine.consensus).  permuted=False keeps chain order in the draws.
+
+        Raises stark_amd._lib.LinAlgError when a shard holds too few draws for
+        its covariance to be invertible: each shard needs more than P draws, i.e.
+        (iter - warmup) * chains > P (P = the model's parameters + lp__; with separate_lp the
+        parameters alone).  The reference's np.linalg.inv returns rounding noise there instead
+        (DESIGN.md section 9)."""
         kwargs = self._defaults(kwargs)
         parts = _rdd.partitions_of(self.rdd)
         subposteriors = self._run_distributed(parts, **kwargs)

@@ -194,6 +194,43 @@ def test_combine_rank_deficient_covariance(ctx, golden, P):
     assert np.isfinite(blk).all()
 
 
+def test_combine_correlated_full_rank_covariance(ctx, orc):
+    """A full-rank covariance with a near-collinear parameter pair (1 - R^2 ~ 1e-12, condition
+    number ~1e12) is inverted, not reported singular: numpy's inv (the reference's combine) returns
+    a usable inverse there, so the GPU combine must too (the singular-pivot threshold
+    is P eps on the unit-diagonal matrix, the rounding level of the elimination)."""
+    from stark_amd import engine
+    rng = np.random.default_rng(21)
+    P, S = 6, 4000
+    draws = []
+    for s in range(3):
+        x = rng.normal(size=(P, S))
+        x[1] = x[0] + 1e-6 * rng.normal(size=S)       # corr(x0, x1) = 1 - 5e-13
+        draws.append(x + rng.normal(size=(P, 1)))
+    c = np.cov(draws[0])
+    assert np.linalg.cond(c) > 1e11
+    ref = orc.consensus_combine_ref(draws)
+    out, used = engine.consensus(draws, ctx)
+    assert used.all() and np.isfinite(out).all()
+    # the weighted average of near-collinear rows is conditioned like W itself: agree to cond * eps
+    np.testing.assert_allclose(out, ref, rtol=0, atol=1e-3 * np.abs(ref).max())
+
+
+def test_combine_device_mismatch_is_refused(ctx):
+    """Device draws on another device than the context's are refused in Python, before the
+    library would dereference them without peer access; the C-ABI itself stages such
+    pointers through hipMemcpyAsync(Default) (capi.hip is_device_ptr checks the device)."""
+    import torch
+    from stark_amd import engine
+
+    class OtherDevice:              # a context on another device: the check fires before any call
+        device = ctx.device + 1
+        _h = None
+    dev_in = torch.zeros((2, 3, 10), dtype=torch.float64, device=f"cuda:{ctx.device}")
+    with pytest.raises(ValueError, match="context"):
+        engine.consensus(dev_in, OtherDevice())
+
+
 def test_combine_device_draws_match_host(ctx):
     """Device-resident draws (a [shards, P, S] cuda tensor, as dist.all_gather_partitions(...,
     as_tensor=True) returns them) combine where they lie, bit-identical to the host-buffer path."""

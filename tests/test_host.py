@@ -108,6 +108,17 @@ def test_sampling_config_mapping():
 
 
 # ---------------------------------------------------------------- RDD shim
+
+def test_sampling_config_refuses_csv_output():
+    """pystan's sample_file / diagnostic_file write Stan CSV; this build returns draws in memory
+    and says so instead of silently dropping the keyword (missing item 4)."""
+    from stark_amd.stark import sampling_config
+    datas = [{"J": 2, "y": [1.0, 2.0], "sigma": [1.0, 1.0]}]
+    for k in ("sample_file", "diagnostic_file"):
+        with pytest.raises(NotImplementedError, match=k):
+            sampling_config("schools", datas, iter=20, chains=1, seed=1, **{k: "/tmp/x.csv"})
+    assert sampling_config("schools", datas, iter=20, chains=1, seed=1, sample_file=None)["num_samples"] == 10
+
 def test_local_rdd_semantics():
     from stark_amd.rdd import LocalContext
     sc = LocalContext()
