@@ -84,6 +84,8 @@ def parse():
     p.add_argument("--seed", type=int, default=20240)
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-schools", action="store_true",
+                   help="skip the configs[1] sub-record (8-schools x 4096 chains, Stan defaults; ~2 s)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "sweep_pmc.json"))
     return p.parse_args()
 
@@ -460,10 +462,10 @@ def main():
                         "the full-data posterior (MAP + inverse Hessian of the GPU gradient, tools/laplace.py)")
 
     # ---- roofline of the dominant kernel (the data sweep)
-    # C = 16: k_sweepe (d = 50, 100) or k_sweepm, X.[beta_1..beta_16] on fp64 MFMA;
+    # C = 16: k_sweep16, X.[beta_1..beta_16] on fp64 MFMA;
     # C <= 4: k_sweep3 (VALU), bound by HBM.
     mfma = a.chains == 16
-    kname = ("k_sweepe" if a.d in (50, 100) else "k_sweepm") if mfma else "k_sweep3"
+    kname = "k_sweep16" if mfma else "k_sweep3"
     ybytes = 4 if a.family == "logistic" else 8
     fam = "LOGREG" if a.family == "logistic" else "LINREG"
     bytes_per_shard = rows_per_shard * (8 * a.d + ybytes)   # X fp64 + y (int32 / fp64), once per sweep
@@ -518,6 +520,17 @@ def main():
             cpu.update(cpu_combine(allp))
         except Exception as e:          # the GPU line is still printed
             cpu = {"error": repr(e)}
+    schools = None
+    if not a.no_schools:               # BASELINE configs[1] (example/stark_ex.py 8-schools, 4096 chains), rank 0
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import bench_schools
+            schools = bench_schools.run(ctx=ctx)
+            schools["note"] = ("BASELINE configs[1]: 8-schools (example/stark_ex.py data, example/schools.stan) with "
+                               "4096 NUTS chains, Stan defaults (1000 warmup + 1000 draws), fused kernel; run on rank 0 "
+                               "after the timed window (tools/bench_schools.py)")
+        except Exception as e:          # the main line is still printed
+            schools = {"error": repr(e)}
     line = {
         "metric": f"gradient evals/sec (whole node), {a.family} regression N={a.rows:.0e} d={a.d}".replace("e+0", "e"),
         "value": value,
@@ -557,6 +570,7 @@ def main():
         "rows_x_chains_per_sec": grads * rows_per_shard / elapsed,
         "roofline": roof,
         "cpu_baseline": cpu,
+        "configs1_schools": schools,
         "combine": {"gpu_ms": float(np.median(comb_ms[1:])), "gpu_ms_min": min(comb_ms[1:]),
                     "gpu_ms_first_call": comb_ms[0], "host_buffers_ms": comb_host_ms, "shards": a.shards, "P": P,
                     "draws": C * n_post, "all_gather_ms": 1e3 * t_gather,

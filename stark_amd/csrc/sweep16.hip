@@ -1,0 +1,398 @@
+// The 16-chain regression sweep (C = 16, any d <= 128): log density + gradient of the 16
+// chains of a shard in ONE pass over the shard's rows, on the fp64 MFMA.
+//
+// Replaces the gradient Stan's reverse-mode autodiff computes for every leapfrog inside
+// `sm.sampling` (stark/stark.py:48) for the regression programs (oracle: orc_logreg_lpgrad /
+// orc_linreg_lpgrad).  With 16 chains sharing a shard, X . [beta_1 .. beta_16] is a dense GEMM
+// (8 flop per byte of X at d = 100) and the sweep is bound by the fp64 pipe at the clock the
+// chip holds under it, not by HBM: every vector instruction takes the issue slot an fp64 MFMA
+// needs (tools/valu_mix.hip), so the design goal is the fewest vector instructions per row
+// (DESIGN.md section 3).
+//
+// Workgroup = 4 waves (two workgroups per CU: two waves per SIMD).  The shard is cut into G
+// chunks that depend only on (n, d); wave w owns the 16-row sub-tiles u = w, w + 4, ... of its
+// chunk.  Per sub-tile:
+//   DMA       16 rows of X and their y, `buffer_load_dwordx4 ... lds` (nt: X is read once per
+//             sweep) into the wave's LDS slot;
+//   forward   eta[16 rows][16 chains] on v_mfma_f64_16x16x4: k-step s, lane group lh = lane>>4
+//             takes column lh KF + s of row lane&15 (A) and beta_{lane&15} at that column (B,
+//             from the block's beta image or registers); KF = ceil(d/4) k-steps, the
+//             accumulator starts at alpha;
+//   release   the backward's A operands, the last <= 4 columns and y move to registers, the
+//             slot takes the DMA of the next sub-tile;
+//   residual  on the MFMA output registers (lane: rows lh + 4i, chain lane&15) -- logistic:
+//             logit_resid4 below; linear: z = (y - eta)/sigma;
+//   backward  G[16 cols][16 chains] += X_tile^T . d_eta: the D layout of the forward is the B
+//             layout of the backward (k-step s = rows 4s..4s+3 = register s), one MFMA per
+//             (16-column tile, k-step); a last tile of <= 4 columns runs on the VALU (16 FMAs
+//             instead of 4 mostly-padding MFMAs).
+// Chunk partials are summed in chunk order by k_sweep_reduce (sweep.hip): the gradient is
+// bitwise independent of how many shards share a launch or which GPU runs a shard.
+#include "sweep_common.h"
+#include <math.h>
+#include <algorithm>
+
+namespace stk {
+
+// exp table: T_j = 2^(j/1024), j < 1024 (8 KB of LDS per workgroup)
+constexpr int EX_TAB = 1024;
+__device__ void exp_table_init(double* tab) {
+  for (int i = threadIdx.x; i < EX_TAB; i += blockDim.x) tab[i] = exp2((double)i / (double)EX_TAB);
+}
+
+// Logistic residual v4: Stan 2.19's bernoulli_logit term and its derivative for one (row,
+// chain), t = (2y - 1) eta:
+//   t > 20:   lt = -exp(-t),             dv/sgn = exp(-t)
+//   t < -20:  lt = t,                    dv/sgn = 1
+//   else:     lt = -log1p(exp(-t)),      dv/sgn = exp(-t) / (exp(-t) + 1)
+// computed branch-free from e = exp(-|t|) as lt = min(t, 0) - log1p(e), dv/sgn = (t < 0 ?
+// 1/(1+e) : e/(1+e)); above 20 the smooth form differs from Stan's by <= e^2/2 < 2.2e-18.
+// The kernel works with s = -t = (1 - 2y) eta, whose sign bit is eta's plus y << 31 (one
+// v_lshl_add_u32: adding 2^31 to the high word flips the sign), and returns -dv the same way;
+// the kernel negates the gradient sums once at the end.
+//
+// The log is not taken per element.  Per lane (one chain) the kernel keeps
+//   lm = sum (t - |t|)              = 2 sum min(t, 0), exact per term, a NaN eta stays NaN
+//   sp = prod (1 + e) - 1           one fma per element: sp <- sp (1 + e) + e
+// and adds log1p(sp) to the lane's lp every 64 sub-tiles (256 elements: 1 + sp < 2^256, and
+// every step adds at most eps of relative error to 1 + sp, so log1p(sp) is off by <= 256 eps
+// absolute); lp = lm/2 - sum log1p(sp).  Rows with e below eps are summed exactly (1 + e = 1,
+// sp += e).  Against residual v3 this drops the table log1p (its index, two LDS reads, a degree-4
+// polynomial) and the per-element lp terms: ~27 instead of ~43 vector instructions per element.
+//   exp(-a), a = min(|t|, 700): n = rint(-a 1024/ln2) by the 1.5 2^52 trick, r = -a - n ln2/1024
+//   (|r| <= ln2/2048; ln2/1024 rounded once: |error of r| <= n ulp(ln2/1024)/2, 1.6e-15 relative at
+//   a = 20), e^r by a fitted degree-3 polynomial (relative error 9.4e-17), times T_{n mod 1024}, times
+//   2^{n div 1024} by v_ldexp_f64 -- whose exponent is -1100 for t < -20, making e = 0: then
+//   lt = min(t, 0) = t and dv/sgn = 1/(1 + 0) = 1 exactly, Stan's lower branch;
+//   1/(1 + e): v_rcp_f64 + one Newton step (11 ulp, tools/rcp_acc.hip).
+__device__ __forceinline__ double fmin_abs(double x, double c) {   // min(|x|, c), NaN x -> c
+  // one v_min_f64 with the abs modifier (fmin() adds a canonicalising v_max_f64 in IEEE mode)
+  double r;
+  asm("v_min_f64 %0, |%1|, %2" : "=v"(r) : "v"(x), "s"(c));
+  return r;
+}
+__device__ __forceinline__ double logit_resid4(double eta, uint32_t y, const double* tab, double& lm, double& sp) {
+  constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
+  constexpr double INV_L = 1477.3197218702985;            // 1024 / ln 2
+  constexpr double L = 0.0006769015435155716;             // ln 2 / 1024
+  constexpr double C2 = 0.5000000039583942, C3 = 0.16666666713444417;   // e^r on |r| <= ln2/2048 (fit)
+  const uint64_t eb = __builtin_bit_cast(uint64_t, eta);
+  const double s = __builtin_bit_cast(double, (eb & 0xFFFFFFFFull) | ((uint64_t)((y << 31) + (uint32_t)(eb >> 32)) << 32));
+  const double a = fmin_abs(s, 700.0);                    // |s| = |eta|; NaN -> 700 (the NaN stays in lm)
+  const double sn = fma(-a, INV_L, MAGIC);
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
+  const double n = sn - MAGIC;
+  const double r = fma(-n, L, -a);
+  const double p = fma(fma(fma(C3, r, C2), r, 1.0), r, 1.0);
+  const int ke = (s > 20.0) ? -1100 : (ni >> 10);         // Stan's lower cutoff (t < -20): e = 0
+  const double e = __builtin_amdgcn_ldexp(tab[ni & (EX_TAB - 1)] * p, ke);
+  const double u = 1.0 + e;
+  double ri = __builtin_amdgcn_rcp(u);
+  ri = fma(ri, fma(-u, ri, 1.0), ri);
+  const double w = e * ri;
+  const uint64_t sb = __builtin_bit_cast(uint64_t, s);
+  const uint32_t spos = (uint32_t)((int32_t)(sb >> 32) >> 31);   // ~0u when s < 0, i.e. t > 0
+  const uint64_t dvp = __builtin_bit_cast(uint64_t, blend(spos, w, ri));   // dv/sgn
+  lm += -s - fabs(s);                                     // t - |t|
+  sp = fma(sp, u, e);
+  return __builtin_bit_cast(double, (dvp & 0xFFFFFFFFull) | ((uint64_t)((y << 31) + (uint32_t)(dvp >> 32)) << 32));   // -dv
+}
+
+// Geometry of k_sweep16 for a given d (host and device).
+struct S16Geom {
+  int KF, JT, REM, JTM;
+  bool VREM;
+};
+__host__ __device__ constexpr S16Geom s16_geom(int KF) {
+  const int JT = (KF + 3) / 4;                  // 16-column tiles covering 4 KF >= d columns
+  const int REM = 4 * KF - 16 * (JT - 1);       // columns of the last tile (d has up to 3 fewer)
+  const bool VREM = REM <= 4;                   // <= 4: the VALU does the last tile
+  return S16Geom{KF, JT, REM, VREM ? JT - 1 : JT, VREM};
+}
+// d > 108 (KF >= 28): the beta image no longer fits next to the slots at two workgroups per CU,
+// so beta is held in registers, and the backward's A operands (which would not fit in registers
+// beside it) are read from the slot, which is then released after the backward instead of after
+// the forward (the next DMA's latency is covered by the SIMD's other wave only).
+__host__ __device__ constexpr bool s16_breg(int KF) { return KF >= 28; }
+constexpr int S16_FLUSH = 64;                   // sub-tiles between log1p flushes (4 elements each)
+
+template <int FAM, int KF, bool BREG = s16_breg(KF), int NACC = 2>
+__global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
+  constexpr S16Geom g = s16_geom(KF);
+  constexpr int C = SM_C, NW = SM_W, JTM = g.JTM, KP = 4 * KF, KB = KP + 2;
+  constexpr bool LOGI = FAM == STK_LOGREG;
+  constexpr bool PRE = !BREG;                  // early release: backward operands into registers
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + 63) / 64;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * 64, r1 = std::min<int64_t>(sh.n, t1 * 64);
+  const int nrows = (int)(r1 - r0);
+  const int nsub = (nrows + SM_R - 1) / SM_R;
+  const int mine = nsub > w ? (nsub - w + NW - 1) / NW : 0;   // own sub-tiles u = w + NW k
+  constexpr int YB = LOGI ? 4 : 8;
+  const int SBX = SM_R * d * 8;
+  const int SS = sweepm_slot_bytes(d);
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const slot = reinterpret_cast<char*>(lds) + (size_t)w * SS;
+  double* const bimg = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);   // [16][KB]
+  double* const tab = bimg + (BREG ? 0 : C * KB);
+  double* const xst = tab + (LOGI ? EX_TAB : 0) + w * 64;      // the last tile's <= 4 columns x 16 rows
+  if constexpr (LOGI) exp_table_init(tab);
+  const double* qs = A.q + (size_t)shard * C * A.Dp;
+  double bf[BREG ? KF : 1];
+  if constexpr (BREG) {
+#pragma unroll
+    for (int s = 0; s < KF; ++s) {
+      const int col = lh * KF + s;
+      bf[s] = col < d ? qs[(size_t)lr * A.Dp + 1 + col] : 0.0;
+    }
+  } else {
+    for (int i = tid; i < C * KP; i += NW * 64) {
+      const int c = i / KP, col = i % KP;
+      bimg[c * KB + col] = col < d ? qs[(size_t)c * A.Dp + 1 + col] : 0.0;
+    }
+  }
+  const double alpha = qs[(size_t)lr * A.Dp];
+  const double inv_s = LOGI ? 0.0 : exp(-qs[(size_t)lr * A.Dp + d + 1]);
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0xF70);
+
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
+  const void* ybase = LOGI ? (const void*)(sh.yi + r0) : (const void*)(sh.y + r0);
+  const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(ybase, (int64_t)nrows * YB);
+  const int nx = (SBX + 1023) >> 10;
+  const int last_lanes = (SBX - ((nx - 1) << 10)) >> 4;
+  auto issue = [&](int k) {           // 1 KiB per DMA instruction, aux = 2 (nt)
+    const int u = w + NW * k;
+    const int xoff = u * SBX;
+    for (int j = 0; j < nx - 1; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(slot + j * 1024), 16, lane * 16, xoff + j * 1024, 0, 2);
+    if (lane < last_lanes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(slot + (nx - 1) * 1024), 16, lane * 16,
+                                               xoff + (nx - 1) * 1024, 0, 2);
+    if (lane < SM_R * YB / 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_vptr)(slot + SBX), 4, lane * 4, u * SM_R * YB, 0, 2);
+  };
+
+  dbl4 gacc[JTM > 0 ? JTM : 1];
+#pragma unroll
+  for (int t = 0; t < JTM; ++t) gacc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double gv[4] = {0.0, 0.0, 0.0, 0.0};
+  double lm = 0.0, sp = 0.0, ll = 0.0, ga = 0.0;   // logistic lp pieces (linear: lm = sum z^2)
+  const double* xs = reinterpret_cast<const double*>(slot);
+  const double* brow = bimg + lr * KB + lh * KF;
+  const double* xrow = xs + lr * d;
+
+  if (mine > 0) issue(0);
+  for (int k = 0; k < mine; ++k) {
+    __builtin_amdgcn_s_waitcnt(0xF70);                 // vmcnt(0): sub-tile k landed
+    __builtin_amdgcn_sched_barrier(0);
+    const int rv = std::min(SM_R, nrows - SM_R * (w + NW * k));
+    // ---- forward: eta[row lh + 4i][chain lr], starting from alpha
+    dbl4 ea[NACC];
+    ea[0] = dbl4{alpha, alpha, alpha, alpha};
+#pragma unroll
+    for (int i = 1; i < NACC; ++i) ea[i] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < KF; ++s) {
+      const double b = BREG ? bf[s] : brow[s];
+      ea[s % NACC] = mfma_f64(xrow[std::min(lh * KF + s, d - 1)], b, ea[s % NACC]);
+    }
+    // ---- everything else the sub-tile needs from the slot, into registers; then release it
+    double xa[4][PRE && JTM > 0 ? JTM : 1];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < JTM; ++t) xa[s][t] = xs[(lh + 4 * s) * d + std::min(16 * t + lr, d - 1)];
+    }
+    if constexpr (g.VREM) xst[lane] = xs[(lane >> 2) * d + std::min(16 * JTM + (lane & 3), d - 1)];
+    uint32_t ym[4];
+    double yv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (LOGI)   // y in {0, 1}
+        ym[i] = *reinterpret_cast<const uint32_t*>(slot + SBX + (lh + 4 * i) * 4);
+      else
+        yv[i] = *reinterpret_cast<const double*>(slot + SBX + (lh + 4 * i) * 8);
+    }
+    if constexpr (PRE) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);              // lgkmcnt(0): the slot is free
+      __builtin_amdgcn_sched_barrier(0);
+      if (k + 1 < mine) issue(k + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    dbl4 eta4 = ea[0];
+#pragma unroll
+    for (int i = 1; i < NACC; ++i) eta4 += ea[i];
+
+    // ---- residual (raised wave priority: the dependent chain goes first, the partner wave's
+    // MFMAs fill its gaps; +1.5 % in round 3's A/B)
+    double de[4];
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(2);
+    if (rv == SM_R) {                                  // full sub-tile: no masks
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (LOGI) {
+          de[i] = logit_resid4(eta4[i], ym[i], tab, lm, sp);
+        } else {
+          const double z = (yv[i] - eta4[i]) * inv_s;
+          lm = fma(z, z, lm);
+          de[i] = z * inv_s;
+        }
+        ga += de[i];
+      }
+    } else {                                           // a chunk's last sub-tile
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool valid = lh + 4 * i < rv;
+        double lm2 = lm, sp2 = sp, dv;
+        if constexpr (LOGI) {
+          dv = logit_resid4(eta4[i], ym[i], tab, lm2, sp2);
+        } else {
+          const double z = (yv[i] - eta4[i]) * inv_s;
+          lm2 = fma(z, z, lm);
+          dv = z * inv_s;
+        }
+        lm = valid ? lm2 : lm;
+        sp = valid ? sp2 : sp;
+        de[i] = valid ? dv : 0.0;
+        ga += de[i];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- backward
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < JTM; ++t)
+        gacc[t] = mfma_f64(PRE ? xa[s][t] : xs[(lh + 4 * s) * d + std::min(16 * t + lr, d - 1)], de[s], gacc[t]);
+    if constexpr (g.VREM) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const dbl2* p = reinterpret_cast<const dbl2*>(xst + (lh + 4 * i) * 4);
+        const dbl2 a0 = p[0], a1 = p[1];
+        gv[0] = fma(a0.x, de[i], gv[0]);
+        gv[1] = fma(a0.y, de[i], gv[1]);
+        gv[2] = fma(a1.x, de[i], gv[2]);
+        gv[3] = fma(a1.y, de[i], gv[3]);
+      }
+    }
+    if constexpr (!PRE) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);              // lgkmcnt(0): the slot is free
+      __builtin_amdgcn_sched_barrier(0);
+      if (k + 1 < mine) issue(k + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (LOGI) {
+      if ((k % S16_FLUSH) == S16_FLUSH - 1) {
+        ll += log1p(sp);
+        sp = 0.0;
+      }
+    }
+  }
+  double lpa;
+  if constexpr (LOGI) {   // the residual returned -dv: negate the gradient sums once
+    lpa = 0.5 * lm - (ll + log1p(sp));
+    ga = -ga;
+#pragma unroll
+    for (int t = 0; t < JTM; ++t) gacc[t] = -gacc[t];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) gv[jj] = -gv[jj];
+  } else {
+    lpa = lm;
+  }
+
+  // ---- fixed-order block reduction -> one partial row per chain
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __syncthreads();
+  double* red = lds;                                   // [NW][JT*16 columns][16 chains]
+  constexpr int JC = g.JT * 16;
+#pragma unroll
+  for (int t = 0; t < JTM; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[((size_t)w * JC + 16 * t + lh + 4 * i) * 16 + lr] = gacc[t][i];
+  double* red2 = red + (size_t)NW * JC * 16;           // [NW][64 lanes][lp, g_alpha]
+  red2[(size_t)tid * 2 + 0] = lpa;
+  red2[(size_t)tid * 2 + 1] = ga;
+  double* red3 = red2 + (size_t)NW * 64 * 2;           // VREM: [NW][4 lh][4 jj][16 chains]
+  if constexpr (g.VREM) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) red3[((size_t)(w * 4 + lh) * 4 + jj) * 16 + lr] = gv[jj];
+  }
+  __syncthreads();
+  double* out = A.partial + ((size_t)shard * A.Gs + chunk) * C * A.PW;
+  const int jv = 16 * JTM;                             // first column summed from red3
+  for (int i = tid; i < C * d; i += NW * 64) {
+    const int c = i / d, j = i % d;
+    double v = 0.0;
+    if (j < jv) {
+      for (int ww = 0; ww < NW; ++ww) v += red[((size_t)ww * JC + j) * 16 + c];
+    } else {
+      for (int ww = 0; ww < NW; ++ww)
+        for (int h = 0; h < 4; ++h) v += red3[((size_t)(ww * 4 + h) * 4 + (j - jv)) * 16 + c];
+    }
+    out[(size_t)c * A.PW + 1 + j] = v;
+  }
+  if (tid < 2 * C) {          // chain c: lanes h*16 + c of every wave, in (wave, h) order
+    const int c = tid >> 1, kind = tid & 1;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww)
+      for (int h = 0; h < 4; ++h) v += red2[(size_t)(ww * 64 + h * 16 + c) * 2 + kind];
+    out[(size_t)c * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
+}
+
+}  // namespace stk
+
+using namespace stk;
+
+// LDS bytes of k_sweep16 at d (the main loop's slots + beta image + table + remainder scratch,
+// or the block reduction's area, whichever is larger).
+size_t stk_sweep16_lds_bytes(int family, int d) {
+  const int KF = (d + 3) / 4;
+  const S16Geom g = s16_geom(KF);
+  size_t main = (size_t)SM_W * sweepm_slot_bytes(d) + (s16_breg(KF) ? 0 : (size_t)SM_C * (4 * KF + 2) * 8) +
+                (family == STK_LOGREG ? EX_TAB * 8 : 0) + (size_t)SM_W * 64 * 8;
+  const size_t red = ((size_t)SM_W * g.JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * 8;
+  return std::max(main, red);
+}
+
+template <int FAM, int KF>
+static hipError_t go16(const SweepArgs& A, int nblocks, size_t lds, hipStream_t st) {
+  auto kern = k_sweep16<FAM, KF>;
+  if (const hipError_t e = allow_big_lds((const void*)kern)) return e;
+  hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A);
+  return hipGetLastError();
+}
+
+template <int FAM>
+static hipError_t launch16(const SweepArgs& A, int d, int nblocks, size_t lds, hipStream_t st) {
+  switch ((d + 3) / 4) {
+#define S16_CASE(K) case K: return go16<FAM, K>(A, nblocks, lds, st);
+    S16_CASE(1) S16_CASE(2) S16_CASE(3) S16_CASE(4) S16_CASE(5) S16_CASE(6) S16_CASE(7) S16_CASE(8)
+    S16_CASE(9) S16_CASE(10) S16_CASE(11) S16_CASE(12) S16_CASE(13) S16_CASE(14) S16_CASE(15) S16_CASE(16)
+    S16_CASE(17) S16_CASE(18) S16_CASE(19) S16_CASE(20) S16_CASE(21) S16_CASE(22) S16_CASE(23) S16_CASE(24)
+    S16_CASE(25) S16_CASE(26) S16_CASE(27) S16_CASE(28) S16_CASE(29) S16_CASE(30) S16_CASE(31) S16_CASE(32)
+#undef S16_CASE
+  }
+  return hipErrorInvalidValue;
+}
+
+bool stk_sweep16_supported(int d) { return d >= 1 && d <= 128; }
+
+hipError_t stk_launch_sweep16(int family, const SweepArgs& A, int d, int nblocks, size_t lds, hipStream_t st) {
+  if (family == STK_LOGREG) return launch16<STK_LOGREG>(A, d, nblocks, lds, st);
+  if (family == STK_LINREG) return launch16<STK_LINREG>(A, d, nblocks, lds, st);
+  return hipErrorInvalidValue;
+}

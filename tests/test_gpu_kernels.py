@@ -39,6 +39,11 @@ def test_schools_lpgrad(ctx, orc):
                                    (1, 1, 16), (7, 3, 16), (1000, 100, 16), (4097, 50, 16), (333, 128, 16),
                                    (65, 104, 20), (20000, 100, 16), (64, 65, 16), (5000, 2, 16), (129, 17, 16),
                                    (333, 129, 16), (3, 100, 16), (9, 50, 16), (100003, 100, 16),
+                                   # k_sweep16 over the d <= 128 table: odd d, the VALU last tile (d = 99, 113,
+                                   # 116), beta in registers with the late slot release (d > 108), and chunks of
+                                   # > 64 sub-tiles per wave (the in-loop log1p flush of residual v4: n > 2.1e6)
+                                   (500, 99, 16), (300, 113, 16), (300, 116, 16), (200, 127, 16), (64, 110, 16),
+                                   (1000, 33, 16), (3000000, 4, 16), (2200000, 17, 16),
                                    # v5 two-pass fp64 MFMA GEMMs (64 chains; 70 = two batches)
                                    (1, 1, 64), (7, 3, 64), (4097, 50, 64), (333, 129, 64), (257, 300, 64),
                                    (1000, 1000, 64), (130, 1001, 70), (5000, 100, 64)])
@@ -69,11 +74,12 @@ def test_regression_lpgrad(ctx, orc, family, n, d, C):
 
 
 @pytest.mark.parametrize("scale", [30.0, 1e3, 1e8, 1e150])
-@pytest.mark.parametrize("n,d,C", [(2000, 100, 16), (999, 50, 16), (300, 40, 16), (500, 100, 64), (400, 60, 4)])
+@pytest.mark.parametrize("n,d,C", [(2000, 100, 16), (999, 50, 16), (300, 40, 16), (300, 99, 16), (300, 113, 16),
+                                   (500, 100, 64), (400, 60, 4)])
 def test_logistic_lpgrad_extreme_eta(ctx, orc, scale, n, d, C):
     """|eta| from ~1 to ~1e151 (NUTS step-size probes from a dispersed init reach such points):
     Stan's +-20 cutoffs -- lt = t, dv = +-1 below, lt ~ -exp(-t) ~ 0 above -- through the
-    table-driven residual of k_sweepe / k_sweepm / pass F (|t| is clamped at 700 before the
+    table-driven residuals of k_sweep16 (v4) and pass F (v3) (|t| is clamped at 700 before the
     exp) and the VALU sweeps, vs the oracle."""
     from stark_amd import engine
     rng = np.random.default_rng(int(scale) % 1000 + n)

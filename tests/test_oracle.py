@@ -169,3 +169,28 @@ def test_residual_v3_emulation_accuracy():
     low = t < -20
     assert np.array_equal(lt[low], t[low]) and np.all(dv[low] == 1.0)
     assert np.isnan(R.resid3(np.array([np.nan]))[0][0])
+
+
+def test_residual_v4_emulation_accuracy():
+    """The design of k_sweep16's logistic residual v4 (sweep16.hip: logit_resid4 -- 1024-entry exp
+    table, fitted degree-3 polynomial, ln2/1024 rounded once, Stan's lower cutoff by a -1100 ldexp
+    exponent, and the log terms summed as log1p of a per-lane running product flushed every 256
+    elements), emulated in numpy by tools/residual_v3_accuracy.py, against Stan's bernoulli_logit
+    term in long double: the lp sum of 2e5 uniform t in [-25, 25] and of a stretch where every e is
+    below eps (t > 37: the product must still add them) within 1e-14 relative, dv within 4e-15
+    relative away from the cutoff bands, exactly 1 below -20, a NaN kept in the sum."""
+    import numpy as np
+    from tools import residual_v3_accuracy as R
+    rng = np.random.default_rng(4)
+    for t in (rng.uniform(-25, 25, 200_000), rng.uniform(37, 45, 50_000), rng.uniform(-0.5, 3, 70_001)):
+        lp, dv = R.resid4(t)
+        lr, dr = R.stan(t)
+        ref = float(lr.sum())
+        assert abs(lp - ref) <= 1e-14 * abs(ref), (lp, ref)
+        inner = np.abs(t) < 20
+        if inner.any():
+            assert (np.abs(dv - dr.astype(np.float64)) / dr.astype(np.float64))[inner].max() < 4e-15
+    t = np.linspace(-30, -20.000001, 999)
+    lp, dv = R.resid4(t)
+    assert np.all(dv == 1.0) and abs(lp - float(t.sum())) <= 1e-15 * abs(float(t.sum()))   # lt = t exactly
+    assert np.isnan(R.resid4(np.array([0.5, np.nan, -3.0]))[0])

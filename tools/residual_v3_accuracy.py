@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
-"""Accuracy of k_sweepe's logistic residual v3 (sweep.hip: logit_resid3) emulated in numpy: the
-same operation sequence in float64 with every fma evaluated in long double and rounded once,
-against Stan 2.19's bernoulli_logit term and derivative (+-20 cutoffs) in long double.  Prints
-the worst errors by t-range, the relative error of an lp sum over 2e6 uniform t in [-25, 25],
-and the NaN / +-inf cases.  (The GPU kernel itself is checked against the C oracle within 1e-10
-by tests/test_gpu_kernels.py.)"""
+"""Accuracy of the logistic residuals emulated in numpy -- v3 (sweep.hip: logit_resid3, the 64-chain
+pass F epilogue) and v4 (sweep16.hip: logit_resid4, the 16-chain sweep, with its per-lane
+product accumulation of the log terms) -- the same operation sequences in float64 with every fma
+evaluated in long double and rounded once, against Stan 2.19's bernoulli_logit term and
+derivative (+-20 cutoffs) in long double.  Prints the worst errors by t-range, the relative error
+of an lp sum over 2e6 uniform t in [-25, 25], and the NaN / +-inf cases.  (The GPU kernels
+themselves are checked against the C oracle within 1e-10 by tests/test_gpu_kernels.py.)"""
 import numpy as np
 
 mp = np.longdouble
@@ -46,6 +47,50 @@ def resid3(t, newton=True):
     return lt, dvp
 
 
+# ---- v4 (sweep16.hip: logit_resid4)
+INV_L4, L4 = 1477.3197218702985, 0.0006769015435155716
+C2, C3 = 0.5000000039583942, 0.16666666713444417
+TE4 = np.array([np.float64(mp(2) ** (mp(i) / 1024)) for i in range(1024)])
+
+
+def resid4(t, lanes=64, flush=256):
+    """v4 on t = (2y - 1) eta: returns (lp sum as the kernel forms it, dv/sgn per element).
+    The elements are dealt to `lanes` lanes in order (lane l takes t[l::lanes]); each lane keeps
+    lm = sum(t - |t|) and sp = prod(1 + e) - 1, adding log1p(sp) every `flush` elements."""
+    t = np.asarray(t, np.float64)
+    with np.errstate(invalid="ignore", over="ignore"):
+        a = np.fmin(np.abs(t), 700.0)
+        sn = fma(-a, INV_L4, MAGIC)
+        ni = (sn.view(np.uint64) & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64)
+        n = sn - MAGIC
+        r = fma(-n, L4, -a)
+        p = fma(fma(fma(C3, r, C2), r, 1.0), r, 1.0)
+        ke = np.where(t < -20.0, -1100, ni >> 10).astype(np.int32)
+        e = np.ldexp(TE4[ni & 1023] * p, ke)
+        u = 1.0 + e
+        ri = (1.0 / u) * (1 + 2.2e-16)           # an rcp seed one ulp off
+        ri = fma(ri, fma(-u, ri, 1.0), ri)
+        w = e * ri
+        dvp = np.where(t > 0, w, ri)
+        m = t - np.abs(t)
+    k = -(-len(t) // lanes) * lanes
+    E = np.zeros(k)
+    U = np.ones(k)
+    M = np.zeros(k)
+    E[:len(t)], U[:len(t)], M[:len(t)] = e, u, m
+    E, U, M = E.reshape(-1, lanes), U.reshape(-1, lanes), M.reshape(-1, lanes)
+    lm = M.sum(0)
+    sp = np.zeros(lanes)
+    ll = np.zeros(lanes)
+    for i in range(E.shape[0]):
+        sp = fma(sp, U[i], E[i])
+        if i % flush == flush - 1:
+            ll = ll + np.log1p(sp)
+            sp = np.zeros(lanes)
+    ll = ll + np.log1p(sp)
+    return float((0.5 * lm - ll).sum()), dvp
+
+
 def stan(t):
     t = t.astype(mp)
     with np.errstate(over="ignore"):
@@ -69,6 +114,10 @@ def main():
     print("lp sum over uniform t in [-25, 25]: relative error %.2e" %
           (abs((lt[:n] - lr[:n].astype(np.float64)).sum()) / abs(lr[:n].astype(np.float64).sum())))
     print("t = NaN, +inf, -inf ->", resid3(np.array([np.nan, np.inf, -np.inf])))
+    lp4, dv4 = resid4(t[:n])
+    er4 = np.abs(dv4 - dr[:n].astype(np.float64)) / dr[:n].astype(np.float64)
+    print("v4: lp sum over uniform t in [-25, 25]: relative error %.2e; dv rel err max %.2e" %
+          (abs(lp4 - float(lr[:n].sum())) / abs(float(lr[:n].sum())), er4.max()))
     lt0, dv0 = resid3(t[:n], newton=False)
     print("without the Newton step (rcp seed 1 ulp off): dv rel err max %.2e" %
           (np.abs(dv0 - dr[:n].astype(np.float64)) / dr[:n].astype(np.float64)).max())

@@ -1,16 +1,15 @@
-// A/B of the C = 16 sweep at BASELINE configs[2]'s shape (linear regression, 8 shards x 1.25e6
-// rows, d = 50, 16 chains; 4.0 GB per sweep): the product kernel for d = 50 (k_sweepm with
-// compile-time KF / JT and the VALU remainder columns) against k_sweepe instantiated for d = 50
-// (one 16-row slot per wave, nt DMA, raised priority around the residual), interleaved rounds,
-// plus a parity check of lp / gradient after the chunk reduction.
-// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/sweepe_d50.hip -o tools/_bin/sweepe_d50
-// Run:   tools/_bin/sweepe_d50 [rows_per_shard] [shards] [rounds] [reps]
+// A/B timing of the 16-chain sweep at the bench geometry (BASELINE configs[3]: 8 shards x 1.25e7
+// rows, d = 100, 16 chains; 80.4 GB per sweep; or configs[2]'s d = 50), interleaved rounds so box
+// drift hits every arm, plus parity of every arm against round 3's product kernel (k_sweepe,
+// residual v3) after the chunk reduction.
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/sweep16_ab.hip -o tools/_bin/sweep16_ab
+// Run:   tools/_bin/sweep16_ab [rows_per_shard] [shards] [rounds] [reps] [d] [family 3=logistic 2=linear]
 #include "../stark_amd/csrc/sweep.hip"
-#include "sweep_legacy.hip"
+#include "sweep_variants.hip"
+#include "../stark_amd/csrc/sweep16.hip"
 #include "../stark_amd/csrc/datagen.hip"
 #include <stdarg.h>
 #include <stdio.h>
-#include <algorithm>
 #include <vector>
 
 void stk_set_error(const char* fmt, ...) {
@@ -32,13 +31,25 @@ void stk_set_error(const char* fmt, ...) {
 
 using namespace stk;
 
+struct Arm {
+  const char* name;
+  const void* kern;
+  size_t lds;
+  std::vector<float> ms;
+};
+
 int main(int argc, char** argv) {
-  const int64_t rows = argc > 1 ? atoll(argv[1]) : 1250000;
+  const int64_t rows = argc > 1 ? atoll(argv[1]) : 12500000;
   const int nsh = argc > 2 ? atoi(argv[2]) : 8;
-  const int rounds = argc > 3 ? atoi(argv[3]) : 5;
-  const int reps = argc > 4 ? atoi(argv[4]) : 50;
-  constexpr int d = 50, C = 16, KF = 13, JT = 4;
-  const int Dp = (d + 2 + 7) / 8 * 8;
+  const int rounds = argc > 3 ? atoi(argv[3]) : 3;
+  const int reps = argc > 4 ? atoi(argv[4]) : 10;
+  const int d = argc > 5 ? atoi(argv[5]) : 100;
+  const int fam = argc > 6 ? atoi(argv[6]) : STK_LOGREG;
+  const int C = 16, Dp = (d + 2 + 7) / 8 * 8;
+  if (!(d == 100 || d == 50)) {
+    fprintf(stderr, "d must be 100 or 50\n");
+    return 2;
+  }
   hipStream_t st;
   CK(hipStreamCreate(&st));
   std::vector<ShardDev> sh(nsh);
@@ -48,20 +59,23 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&beta_d, sizeof(double) * d));
   CK(hipMemcpy(beta_d, beta.data(), sizeof(double) * d, hipMemcpyHostToDevice));
   for (int s = 0; s < nsh; ++s) {
-    double *X, *y;
+    double* X;
+    int32_t* yi = nullptr;
+    double* yd = nullptr;
     CK(hipMalloc(&X, sizeof(double) * rows * d));
-    CK(hipMalloc(&y, sizeof(double) * rows));
-    CK(stk_launch_gen_shard(X, y, nullptr, rows, d, s * rows, 20240, 0.3, beta_d, 1.0, STK_LINREG, st));
-    sh[s] = ShardDev{X, y, nullptr, nullptr, rows, d, d + 2, d + 3, 0.0, 0.0};
+    if (fam == STK_LOGREG) CK(hipMalloc(&yi, sizeof(int32_t) * rows));
+    else CK(hipMalloc(&yd, sizeof(double) * rows));
+    CK(stk_launch_gen_shard(X, yd, yi, rows, d, s * rows, 20240, 0.0, beta_d, 1.0, fam, st));
+    sh[s] = ShardDev{X, yd, yi, nullptr, rows, d, fam == STK_LOGREG ? d + 1 : d + 2, d + 2};
   }
   ShardDev* sh_d;
   CK(hipMalloc(&sh_d, sizeof(ShardDev) * nsh));
   CK(hipMemcpy(sh_d, sh.data(), sizeof(ShardDev) * nsh, hipMemcpyHostToDevice));
   std::vector<double> qh((size_t)nsh * C * Dp, 0.0);
   for (int g = 0; g < nsh * C; ++g) {
-    qh[(size_t)g * Dp] = 0.3 + 0.01 * ((g % 5) - 2);                 // alpha
+    qh[(size_t)g * Dp] = 0.05 * ((g % 5) - 2);                      // alpha
     for (int j = 0; j < d; ++j) qh[(size_t)g * Dp + 1 + j] = beta[j] * (0.9 + 0.01 * g);
-    qh[(size_t)g * Dp + d + 1] = 0.02 * (g % 7);                       // log sigma
+    if (fam == STK_LINREG) qh[(size_t)g * Dp + d + 1] = 0.1 * (g % 3);   // log sigma
   }
   double *q, *partial, *lp, *grad;
   CK(hipMalloc(&q, sizeof(double) * qh.size()));
@@ -73,38 +87,34 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&lp, sizeof(double) * nsh * C));
   CK(hipMalloc(&grad, sizeof(double) * nsh * C * Dp));
   CK(hipStreamSynchronize(st));
-  const double bytes = (double)nsh * rows * (8.0 * d + 8.0);
+  const double bytes = (double)nsh * rows * (8.0 * d + (fam == STK_LOGREG ? 4.0 : 8.0));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   SweepArgs A{sh_d, q, partial, nullptr, 0, C, Dp, G, LD, d + 2, 0, G, nullptr};
-  // k_sweepe's LDS: the per-wave slots, the beta image [16][4 KF + SE_BPAD], the (unused for the
-  // linear family) table block, the ER / PF scratch; or the block reduction, whichever is larger
-  const size_t lds_e = std::max(
-      (size_t)SM_W * sweepm_slot_bytes(d) + (16 * (4 * KF + SE_BPAD) + LG_TAB + SM_W * 64 + SM_W * 32) * sizeof(double),
-      ((size_t)SM_W * JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * sizeof(double));
-  printf("rows/shard %lld shards %d d %d C %d: G %d LD %d lds %zu (sweepe %zu), %.2f GB per sweep\n", (long long)rows,
-         nsh, d, C, G, LD, lds, lds_e, bytes / 1e9);
-  struct Arm { const char* name; const void* kern; bool m; size_t lds; std::vector<float> ms; };
-  std::vector<Arm> arms = {
-      {"sweepm", (const void*)k_sweepm<STK_LINREG, KF, JT, 0, SM_MINB, true>, true, lds, {}},
-      {"sweepe", (const void*)k_sweepe<STK_LINREG, KF, JT, 0, 1, SE_NACC, 0, 2, 1>, false, lds_e, {}},
-      {"sweepe-p0", (const void*)k_sweepe<STK_LINREG, KF, JT, 0, 1, SE_NACC, 0, 2, 0>, false, lds_e, {}},
-  };
+  const size_t l16 = stk_sweep16_lds_bytes(fam, d);
+  printf("rows/shard %lld shards %d d %d C %d family %d: G %d lds %zu / %zu, %.1f GB per sweep\n", (long long)rows, nsh,
+         d, C, fam, G, lds, l16, bytes / 1e9);
+  std::vector<Arm> arms;
+#define ARMS(F, KF, JT)                                                                      \
+  arms = {{"e3", (const void*)k_sweepe<F, KF, JT, 0, 3, 2, 0, 2, 1>, lds, {}},               \
+          {"s16", (const void*)k_sweep16<F, KF, false, 2>, l16, {}},                         \
+          {"s16n1", (const void*)k_sweep16<F, KF, false, 1>, l16, {}}};
+  if (fam == STK_LOGREG) {
+    if (d == 100) { ARMS(STK_LOGREG, 25, 7) } else { ARMS(STK_LOGREG, 13, 4) }
+  } else {
+    if (d == 100) { ARMS(STK_LINREG, 25, 7) } else { ARMS(STK_LINREG, 13, 4) }
+  }
   for (auto& a : arms) CK(hipFuncSetAttribute(a.kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   auto launch = [&](const Arm& a) {
-    if (a.m)
-      hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs, int)>(const_cast<void*>(a.kern)), dim3(nsh * G),
-                         dim3(SM_W * 64), a.lds, st, A, LD);
-    else
-      hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.kern)), dim3(nsh * G),
-                         dim3(SM_W * 64), a.lds, st, A);
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.kern)), dim3(nsh * G), dim3(256), a.lds,
+                       st, A);
   };
   std::vector<std::vector<double>> res;
   for (size_t k = 0; k < arms.size(); ++k) {
     launch(arms[k]);
     CK(hipGetLastError());
-    CK(stk_launch_sweep_reduce(STK_LINREG, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
+    CK(stk_launch_sweep_reduce(fam, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
     std::vector<double> h((size_t)nsh * C * (Dp + 1));
     CK(hipMemcpyAsync(h.data(), lp, sizeof(double) * nsh * C, hipMemcpyDeviceToHost, st));
     CK(hipMemcpyAsync(h.data() + nsh * C, grad, sizeof(double) * nsh * C * Dp, hipMemcpyDeviceToHost, st));
@@ -116,8 +126,8 @@ int main(int argc, char** argv) {
     for (int i = 0; i < nsh * C; ++i) lpr = std::max(lpr, fabs(res[k][i] - res[0][i]) / fabs(res[0][i]));
     for (size_t i = nsh * C; i < res[0].size(); ++i) gmax = std::max(gmax, fabs(res[0][i]));
     for (size_t i = nsh * C; i < res[0].size(); ++i) gr = std::max(gr, fabs(res[k][i] - res[0][i]) / gmax);
-    printf("parity %s vs sweepm: lp max rel %.3g, grad max |diff| / max|grad| %.3g (lp[0] %.6f)\n", arms[k].name, lpr,
-           gr, res[0][0]);
+    printf("parity %s vs %s: lp max rel %.3g, grad max |diff| / max|grad| %.3g (lp[0] %.6f)\n", arms[k].name,
+           arms[0].name, lpr, gr, res[0][0]);
   }
   for (int r = 0; r < rounds; ++r) {
     for (auto& a : arms) {
@@ -130,7 +140,7 @@ int main(int argc, char** argv) {
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       a.ms.push_back(ms / reps);
-      printf("round %d %-10s %8.4f ms  %7.1f GB/s  %.3f of 8 TB/s\n", r, a.name, ms / reps, bytes / (ms / reps) / 1e6,
+      printf("round %d %-8s %8.3f ms  %7.1f GB/s  %.3f of 8 TB/s\n", r, a.name, ms / reps, bytes / (ms / reps) / 1e6,
              bytes / (ms / reps) / 1e6 / 8000.0);
       fflush(stdout);
     }
@@ -138,7 +148,7 @@ int main(int argc, char** argv) {
   for (auto& a : arms) {
     std::vector<float> v = a.ms;
     std::sort(v.begin(), v.end());
-    printf("median %-10s %8.4f ms  %.3f of 8 TB/s\n", a.name, v[v.size() / 2], bytes / v[v.size() / 2] / 1e6 / 8000.0);
+    printf("median %-8s %8.3f ms  %.3f of 8 TB/s\n", a.name, v[v.size() / 2], bytes / v[v.size() / 2] / 1e6 / 8000.0);
   }
   return 0;
 }

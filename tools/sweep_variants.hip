@@ -4,6 +4,7 @@
 // and slower than k_sweepe; they are kept here, out of libstark_hip.so, for tools/sweep_micro.hip
 // and tools/sweepe_ab.hip only (included after sweep.hip, namespace stk).
 // Build: see tools/sweep_micro.hip.
+#include "sweep_legacy.hip"
 namespace stk {
 
 // v4r: the v4 sub-tile computation with the NEXT sub-tile streamed through registers.
