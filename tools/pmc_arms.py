@@ -20,9 +20,9 @@ XCDS = 8
 
 
 def short(name):
-    m = re.search(r"k_sweepe<([^>]*)>", name)
+    m = re.search(r"(k_sweepe|k_sweep16)<([^>]*)>", name)
     if m:
-        return "k_sweepe<" + m.group(1).replace(" ", "") + ">"
+        return m.group(1) + "<" + m.group(2).replace(" ", "") + ">"
     return name.split("(")[0][:80]
 
 
