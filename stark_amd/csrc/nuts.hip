@@ -30,6 +30,8 @@
 
 namespace stk {
 
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
 
 // Lane exchange of a double by DPP (VALU, a few cycles; __shfl is a ds_bpermute round trip).
 // bound_ctrl: an invalid source lane reads 0 -- the old value 0 would give the same, but as an
@@ -98,6 +100,67 @@ __device__ __forceinline__ double log_sum_exp2(double a, double b) {   // stan::
   return b + log1p(exp(a - b));
 }
 
+// ------------------------------------------------------------------ table-driven exp / log1p
+// The fused 8-schools kernel is a serial chain of dependent fp64 operations per leapfrog at one
+// wave per SIMD, and ocml's f64 exp is ~35 vector instructions, log1p ~130 and a log_sum_exp
+// ~180; a leaf takes 1-3 exps and a merge one log_sum_exp.  With a 5 KB table in the workgroup's
+// LDS (MT_N doubles, filled once per launch):
+//   exp_mt(x)       x = n ln2/128 + r (n = rint(x 128/ln2) by the 1.5 2^52 trick, ln2/128 in two
+//                   parts so n L_HI is exact), e^r by its degree-5 Taylor polynomial (|r| <= ln2/256:
+//                   truncation 5e-19), times 2^{(n mod 128)/128} from the table, times 2^{n div 128}
+//                   by v_ldexp_f64; x clamped to [-800, 800] first (0 / inf beyond), NaN kept;
+//   log1p01_mt(e)   e in [0, 1]: j = rint(128 e), rl = e c_j - d_j = (e - j/128) / (1 + j/128)
+//                   (|rl| <= 1/256, exact for j = 0, so a tiny e keeps its relative accuracy),
+//                   log1p(e) = log1p(j/128) + log1p(rl), the latter by its degree-7 Taylor series;
+// about 20 and 14 instructions, errors of 1-2 ulp (tools/nuts_math_accuracy.py).  The recursive CPU
+// twin (libm) and the GPU machine then differ by ulps in log weights and acceptance probabilities,
+// as they already did with ocml's: a multinomial / acceptance decision flips only when the uniform
+// lies within those ulps of the threshold.
+constexpr int MT_E = 128;                    // T_j = 2^(j/128)
+constexpr int MT_L = 129;                    // [c_j, d_j, l_j, 0], j = 0..128
+constexpr int MT_N = MT_E + 4 * MT_L;
+__device__ void mt_init(double* t, int tid, int nthreads) {
+  for (int i = tid; i < MT_N; i += nthreads) {
+    double v;
+    if (i < MT_E) {
+      v = exp2((double)i / (double)MT_E);
+    } else {
+      const int j = (i - MT_E) >> 2, f = (i - MT_E) & 3;
+      v = f == 0 ? 128.0 / (128 + j) : (f == 1 ? (double)j / (128 + j) : (f == 2 ? log1p((double)j / 128.0) : 0.0));
+    }
+    t[i] = v;
+  }
+}
+__device__ __forceinline__ double exp_mt(double x, const double* t) {
+  constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
+  constexpr double INV_L = 184.6649652337873;             // 128 / ln 2
+  constexpr double L_HI = 0.005415212348452769;           // ln2/128 to 32 significant bits
+  constexpr double L_LO = -3.2819649005320973e-13;        // ln2/128 - L_HI
+  const double xc = fmin(fmax(x, -800.0), 800.0);
+  const double sn = fma(xc, INV_L, MAGIC);
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
+  const double n = sn - MAGIC;
+  double r = fma(-n, L_HI, xc);
+  r = fma(-n, L_LO, r);
+  const double p = fma(fma(fma(fma(fma(1.0 / 120.0, r, 1.0 / 24.0), r, 1.0 / 6.0), r, 0.5), r, 1.0), r, 1.0);
+  const double e = __builtin_amdgcn_ldexp(t[ni & (MT_E - 1)] * p, ni >> 7);
+  return x == x ? e : x;
+}
+__device__ __forceinline__ double log1p01_mt(double e, const double* t) {   // e in [0, 1] (NaN kept)
+  const int j = (int)fma(e, 128.0, 0.5);
+  const double* cj = t + MT_E + 4 * j;
+  const dbl2 cd = *reinterpret_cast<const dbl2*>(cj);
+  const double rl = fma(e, cd.x, -cd.y);
+  const double q = fma(fma(fma(fma(fma(fma(1.0 / 7.0, rl, -1.0 / 6.0), rl, 0.2), rl, -0.25), rl, 1.0 / 3.0), rl, -0.5), rl, 1.0);
+  return fma(rl, q, cj[2]);
+}
+__device__ __forceinline__ double log_sum_exp_mt(double a, double b, const double* t) {   // as log_sum_exp2
+  if (a == -INFINITY) return b;
+  if (a == INFINITY && b == INFINITY) return INFINITY;
+  if (a > b) return a + log1p01_mt(exp_mt(b - a, t), t);
+  return b + log1p01_mt(exp_mt(a - b, t), t);
+}
+
 // ------------------------------------------------------------------ model hooks
 // 8 schools (example/schools.stan:1-18): q = (mu, log tau, eta_1..J); returns lp, writes
 // grad lp.  Mirrors oracle orc_schools_lpgrad.
@@ -116,12 +179,14 @@ __device__ __forceinline__ void schools_data(const ShardDev& sh, double (&yc)[NC
     isc[k] = in ? 1.0 / sh.sigma[e - 2] : 1.0;
   }
 }
-template <int NCH, int SEG = WAVE>
+template <int NCH, int SEG = WAVE, bool FM = false>
 __device__ double schools_lpgrad(const double (&yc)[NCH], const double (&isc)[NCH], const double (&q)[NCH],
-                                 double (&glp)[NCH], int lane, int D) {
+                                 double (&glp)[NCH], int lane, int D, const double* mt = nullptr) {
   const double mu = seg_bcast<SEG, 0>(q[0]);
   const double u = seg_bcast<SEG, 1>(q[0]);
-  const double tau = exp(u);
+  double tau;
+  if constexpr (FM) tau = exp_mt(u, mt);
+  else tau = exp(u);
   double lp = 0.0, smu = 0.0, su = 0.0;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
@@ -202,7 +267,7 @@ __device__ __forceinline__ void write_draw(const NutsArgs& A, const ShardDev& sh
 // ------------------------------------------------------------------ the chain
 // SEG: lanes per chain (64: one chain per wave; 16 / 32: 4 / 2 chains packed in a wave, each
 // in its own DPP row(s), D <= SEG).  `lane` is the lane's position inside its segment.
-template <int NCH, int SEG = WAVE>
+template <int NCH, int SEG = WAVE, bool FM = false>
 // (every member is force-inlined: a non-inlined constructor or method receiving `this` puts
 // the whole chain object -- s[], iv[], q, p, g -- in scratch memory; 48.7 -> 26.1 us per step,
 // profiles/r02q_kernel_stats.csv vs r02r_kernel_stats_global.csv)
@@ -222,6 +287,15 @@ struct NutsChain {
   double s[S_COUNT];
   int iv[I_COUNT];
   double q[NCH], p[NCH], g[NCH], im[NCH];
+  const double* mt = nullptr;     // FM: the fused kernel's exp / log1p table in LDS (else ocml)
+  __device__ __forceinline__ double ex(double x) const {
+    if constexpr (FM) return exp_mt(x, mt);
+    else return exp(x);
+  }
+  __device__ __forceinline__ double lse(double a, double b) const {
+    if constexpr (FM) return log_sum_exp_mt(a, b, mt);
+    else return log_sum_exp2(a, b);
+  }
   uint32_t nleap = 0, ndiv = 0;   // leapfrogs / divergent draws since the last flush_counts()
 
   __device__ __forceinline__ NutsChain(const NutsArgs& a, int gid_, int lane_)
@@ -586,7 +660,7 @@ struct NutsChain {
     if (isnan(h)) h = INFINITY;
     if ((h - H0) > 1000.0) IV(I_DIV) = 1;
     IV(I_NLEAP) += 1;
-    S(S_SUMMETRO) += (H0 - h > 0) ? 1.0 : exp(H0 - h);
+    S(S_SUMMETRO) += (H0 - h > 0) ? 1.0 : ex(H0 - h);
     // the leaf as a depth-0 sub-tree
     double c_lsw = H0 - h;
     double c_rho[NCH], c_psb[NCH], c_pse[NCH], c_q[NCH], c_g[NCH], c_pb[NCH];
@@ -610,9 +684,9 @@ struct NutsChain {
       double l_rho[NCH], l_psb[NCH];
       ld(svp(j, SV_RHO), l_rho);
       ld(svp(j, SV_PSB), l_psb);
-      const double lsw_sub = log_sum_exp2(l_lsw, c_lsw);
+      const double lsw_sub = lse(l_lsw, c_lsw);
       const double u = uniform();
-      const bool take_right = (c_lsw > lsw_sub) || (u < exp(c_lsw - lsw_sub));
+      const bool take_right = (c_lsw > lsw_sub) || (u < ex(c_lsw - lsw_sub));
       if (!take_right) {
         ld(svp(j, SV_Q), c_q);
         ld(svp(j, SV_G), c_g);
@@ -679,13 +753,13 @@ struct NutsChain {
     else S(S_VB) = S(S_V);                //  would move them to scratch)
     IV(I_DEPTH) = depth + 1;
     const double u = uniform();
-    if (c_lsw > S(S_LSW) || u < exp(c_lsw - S(S_LSW))) {
+    if (c_lsw > S(S_LSW) || u < ex(c_lsw - S(S_LSW))) {
       st(vp(V_QS), c_q);
       st(vp(V_GS), c_g);
       S(S_VS) = c_V;
       S(S_HS) = c_H;
     }
-    S(S_LSW) = log_sum_exp2(S(S_LSW), c_lsw);
+    S(S_LSW) = lse(S(S_LSW), c_lsw);
     double rho[NCH], psp[NCH], psm[NCH], rho_old[NCH];
     ld(vp(V_RHO), rho);
 #pragma unroll
@@ -833,7 +907,10 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   const size_t nv = (size_t)V_COUNT * A.Dp, ns = (size_t)A.max_depth * stack_vecs(A) * A.Dp;
   const size_t nss = (size_t)A.max_depth * SS_COUNT;
   constexpr size_t nsc = S_COUNT + (I_COUNT + 1) / 2;   // the chain's scalars and counters
-  double* const fl = fl_all + (size_t)seg * (nv + ns + nss + nsc);
+  const size_t per = (nv + ns + nss + nsc + 1) & ~(size_t)1;      // per-chain image, even (table 16-B aligned)
+  double* const fl = fl_all + (size_t)seg * per;
+  double* const mtab = fl_all + (size_t)CPW * per;                   // exp / log1p table (MT_N doubles)
+  mt_init(mtab, (int)threadIdx.x, WAVE);
   double* const lsc = fl + nv + ns + nss;
   int* const liv = (int*)(lsc + S_COUNT);
   double* const gvec = A.vec + (size_t)gid * nv;
@@ -853,7 +930,8 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   }
   __syncthreads();
   if (run) {
-    NutsChain<NCH, SEG> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
+    NutsChain<NCH, SEG, true> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
+    ch.mt = mtab;
     ch.load();
     double yc[NCH], isc[NCH];
     schools_data<NCH, SEG>(ch.sh, yc, isc, lane, ch.D);
@@ -875,7 +953,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
       unsigned long long ngrad = 0;
       while (req && steps < max_steps) {
         double glp[NCH];
-        const double lp = schools_lpgrad<NCH, SEG>(yc, isc, ch.q, glp, lane, ch.D);
+        const double lp = schools_lpgrad<NCH, SEG, true>(yc, isc, ch.q, glp, lane, ch.D, mtab);
         ++steps;
         req = ch.consume(lp, glp, pause_at);
         if (req) ++ngrad;
@@ -935,8 +1013,10 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
 }
 template <int NCH, int CPW, int MINW = 1>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
-  const size_t lds = CPW * sizeof(double) * ((size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp +
-                                             (size_t)A.max_depth * SS_COUNT + S_COUNT + (I_COUNT + 1) / 2);
+  size_t per = (size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp + (size_t)A.max_depth * SS_COUNT +
+               S_COUNT + (I_COUNT + 1) / 2;
+  per += per & 1;                                        // keep the table after the chains 16-B aligned
+  const size_t lds = sizeof(double) * (CPW * per + MT_N);
   if (lds > 64 * 1024) {
     // the attribute is per device (allow_big_lds keys it on the current one); a failure is
     // reported as such rather than as a generic launch failure
@@ -983,11 +1063,7 @@ hipError_t stk_launch_nuts_fused(const NutsArgs& A, int nch, int pause_at, int m
   if (nch == 1) {
     switch (fused_cpw(A)) {
       case 4: return launch_fused_t<1, 4>(A, pause_at, max_steps, st);
-#ifdef STK_FUSED_MINW2   // measurement builds only (tools/gpu): chains_per_wave = 2 at two waves per SIMD
-      case 2: return launch_fused_t<1, 2, 2>(A, pause_at, max_steps, st);
-#else
       case 2: return launch_fused_t<1, 2>(A, pause_at, max_steps, st);
-#endif
       default: return launch_fused_t<1, 1>(A, pause_at, max_steps, st);
     }
   }

@@ -194,3 +194,18 @@ def test_residual_v4_emulation_accuracy():
     lp, dv = R.resid4(t)
     assert np.all(dv == 1.0) and abs(lp - float(t.sum())) <= 1e-15 * abs(float(t.sum()))   # lt = t exactly
     assert np.isnan(R.resid4(np.array([0.5, np.nan, -3.0]))[0])
+
+
+def test_nuts_table_math_emulation_accuracy():
+    """The fused NUTS kernel's table-driven exp / log1p (nuts.hip exp_mt, log1p01_mt), emulated in
+    numpy by tools/nuts_math_accuracy.py: within 3 ulp of long-double references over the ranges
+    the state machine feeds them, with exp's special values (0, inf, NaN) kept."""
+    import numpy as np
+    from tools import nuts_math_accuracy as M
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(-40, 0, 100_000), rng.uniform(-700, 700, 100_000)])
+    assert M.ulps(M.exp_mt(x), np.exp(x.astype(np.longdouble))).max() < 3
+    e = np.concatenate([rng.uniform(0, 1, 100_000), 10.0 ** rng.uniform(-300, 0, 50_000), [0.0, 1.0]])
+    assert M.ulps(M.log1p01_mt(e), np.log1p(e.astype(np.longdouble))).max() < 3
+    sp = M.exp_mt(np.array([-np.inf, np.inf, np.nan, -1000.0, 1000.0]))
+    assert sp[0] == 0 and sp[1] == np.inf and np.isnan(sp[2]) and sp[3] == 0 and sp[4] == np.inf

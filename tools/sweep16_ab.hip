@@ -7,6 +7,7 @@
 #include "../stark_amd/csrc/sweep.hip"
 #include "sweep_variants.hip"
 #include "../stark_amd/csrc/sweep16.hip"
+#include "sweep16_variants.hip"
 #include "../stark_amd/csrc/datagen.hip"
 #include <stdarg.h>
 #include <stdio.h>
@@ -96,10 +97,15 @@ int main(int argc, char** argv) {
   printf("rows/shard %lld shards %d d %d C %d family %d: G %d lds %zu / %zu, %.1f GB per sweep\n", (long long)rows, nsh,
          d, C, fam, G, lds, l16, bytes / 1e9);
   std::vector<Arm> arms;
-#define ARMS(F, KF, JT)                                                                      \
-  arms = {{"e3", (const void*)k_sweepe<F, KF, JT, 0, 3, 2, 0, 2, 1>, lds, {}},               \
-          {"s16", (const void*)k_sweep16<F, KF, false, 2>, l16, {}},                         \
-          {"s16n1", (const void*)k_sweep16<F, KF, false, 1>, l16, {}}};
+#define ARMS(F, KF, JT)                                                                        \
+  arms = {{"s16", (const void*)k_sweep16<F, KF>, l16, {}},                                     \
+          {"e3", (const void*)k_sweepe<F, KF, JT, 0, 3, 2, 0, 2, 1>, lds, {}},                 \
+          {"x-lsa", (const void*)k_sweep16x<F, KF, false, 2, true, false>, l16, {}},           \
+          {"x-lsa-n1", (const void*)k_sweep16x<F, KF, false, 1, true, false>, l16, {}},        \
+          {"x-pair", (const void*)k_sweep16x<F, KF, false, 2, false, true>, l16, {}},          \
+          {"x-lsa-pair", (const void*)k_sweep16x<F, KF, false, 2, true, true>, l16, {}},       \
+          {"x-breg", (const void*)k_sweep16x<F, KF, true, 2, false, false>, l16, {}},          \
+          {"x-breg-lsa", (const void*)k_sweep16x<F, KF, true, 2, true, false>, l16, {}}};
   if (fam == STK_LOGREG) {
     if (d == 100) { ARMS(STK_LOGREG, 25, 7) } else { ARMS(STK_LOGREG, 13, 4) }
   } else {

@@ -1,83 +1,28 @@
-// The 16-chain regression sweep (C = 16, any d <= 128): log density + gradient of the 16
-// chains of a shard in ONE pass over the shard's rows, on the fp64 MFMA.
-//
-// Replaces the gradient Stan's reverse-mode autodiff computes for every leapfrog inside
-// `sm.sampling` (stark/stark.py:48) for the regression programs (oracle: orc_logreg_lpgrad /
-// orc_linreg_lpgrad).  With 16 chains sharing a shard, X . [beta_1 .. beta_16] is a dense GEMM
-// (8 flop per byte of X at d = 100) and the sweep is bound by the fp64 pipe at the clock the
-// chip holds under it, not by HBM: every vector instruction takes the issue slot an fp64 MFMA
-// needs (tools/valu_mix.hip), so the design goal is the fewest vector instructions per row
-// (DESIGN.md section 3).
-//
-// Workgroup = 4 waves (two workgroups per CU: two waves per SIMD).  The shard is cut into G
-// chunks that depend only on (n, d); wave w owns the 16-row sub-tiles u = w, w + 4, ... of its
-// chunk.  Per sub-tile:
-//   DMA       16 rows of X and their y, `buffer_load_dwordx4 ... lds` (nt: X is read once per
-//             sweep) into the wave's LDS slot;
-//   forward   eta[16 rows][16 chains] on v_mfma_f64_16x16x4: k-step s, lane group lh = lane>>4
-//             takes column lh KF + s of row lane&15 (A) and beta_{lane&15} at that column (B,
-//             from the block's beta image or registers); KF = ceil(d/4) k-steps, the
-//             accumulator starts at alpha;
-//   release   the backward's A operands, the last <= 4 columns and y move to registers, the
-//             slot takes the DMA of the next sub-tile;
-//   residual  on the MFMA output registers (lane: rows lh + 4i, chain lane&15) -- logistic:
-//             logit_resid4 below; linear: z = (y - eta)/sigma;
-//   backward  G[16 cols][16 chains] += X_tile^T . d_eta: the D layout of the forward is the B
-//             layout of the backward (k-step s = rows 4s..4s+3 = register s), one MFMA per
-//             (16-column tile, k-step); a last tile of <= 4 columns runs on the VALU (16 FMAs
-//             instead of 4 mostly-padding MFMAs).
-// Chunk partials are summed in chunk order by k_sweep_reduce (sweep.hip): the gradient is
-// bitwise independent of how many shards share a launch or which GPU runs a shard.
-#include "sweep_common.h"
-#include <math.h>
-#include <algorithm>
-
+// Measurement-only variants of the 16-chain sweep k_sweep16 (stark_amd/csrc/sweep16.hip), for
+// tools/sweep16_ab.hip: the same kernel with knobs
+//   BREG / NACC   as the product (beta in registers + late slot release; forward accumulators)
+//   LSA           (y << 31) + hi as ONE v_lshl_add_u32 per use (inline asm; the compiler otherwise
+//                 shares one v_lshlrev_b32 between the two uses and adds twice: 3 instructions)
+//   PAIR          the forward's k-steps 2m, 2m+1 read columns 8m + 2 lh, +1 of X and beta as one
+//                 ds_read_b128 each (needs an even d), instead of two ds_read_b64
+// Included after sweep16.hip (namespace stk).
 namespace stk {
 
-// exp table: T_j = 2^(j/1024), j < 1024 (8 KB of LDS per workgroup)
-constexpr int EX_TAB = 1024;
-__device__ void exp_table_init(double* tab) {
-  for (int i = threadIdx.x; i < EX_TAB; i += blockDim.x) tab[i] = exp2((double)i / (double)EX_TAB);
-}
-
-// Logistic residual v4: Stan 2.19's bernoulli_logit term and its derivative for one (row,
-// chain), t = (2y - 1) eta:
-//   t > 20:   lt = -exp(-t),             dv/sgn = exp(-t)
-//   t < -20:  lt = t,                    dv/sgn = 1
-//   else:     lt = -log1p(exp(-t)),      dv/sgn = exp(-t) / (exp(-t) + 1)
-// computed branch-free from e = exp(-|t|) as lt = min(t, 0) - log1p(e), dv/sgn = (t < 0 ?
-// 1/(1+e) : e/(1+e)); above 20 the smooth form differs from Stan's by <= e^2/2 < 2.2e-18.
-// The kernel works with s = -t = (1 - 2y) eta, whose sign bit is eta's plus y << 31 (one
-// v_lshl_add_u32: adding 2^31 to the high word flips the sign), and returns -dv the same way;
-// the kernel negates the gradient sums once at the end.
-//
-// The log is not taken per element.  Per lane (one chain) the kernel keeps
-//   lm = sum (t - |t|)              = 2 sum min(t, 0), exact per term, a NaN eta stays NaN
-//   sp = prod (1 + e) - 1           one fma per element: sp <- sp (1 + e) + e
-// and adds log1p(sp) to the lane's lp every 64 sub-tiles (256 elements: 1 + sp < 2^256, and
-// every step adds at most eps of relative error to 1 + sp, so log1p(sp) is off by <= 256 eps
-// absolute); lp = lm/2 - sum log1p(sp).  Rows with e below eps are summed exactly (1 + e = 1,
-// sp += e).  Against residual v3 this drops the table log1p (its index, two LDS reads, a degree-4
-// polynomial) and the per-element lp terms: ~27 instead of ~43 vector instructions per element.
-//   exp(-a), a = min(|t|, 700): n = rint(-a 1024/ln2) by the 1.5 2^52 trick, r = -a - n ln2/1024
-//   (|r| <= ln2/2048; ln2/1024 rounded once: |error of r| <= n ulp(ln2/1024)/2, 1.6e-15 relative at
-//   a = 20), e^r by a fitted degree-3 polynomial (relative error 9.4e-17), times T_{n mod 1024}, times
-//   2^{n div 1024} by v_ldexp_f64 -- whose exponent is -1100 for t < -20, making e = 0: then
-//   lt = min(t, 0) = t and dv/sgn = 1/(1 + 0) = 1 exactly, Stan's lower branch;
-//   1/(1 + e): v_rcp_f64 + one Newton step (11 ulp, tools/rcp_acc.hip).
-__device__ __forceinline__ double fmin_abs(double x, double c) {   // min(|x|, c), NaN x -> c
-  // one v_min_f64 with the abs modifier (fmin() adds a canonicalising v_max_f64 in IEEE mode)
-  double r;
-  asm("v_min_f64 %0, |%1|, %2" : "=v"(r) : "v"(x), "s"(c));
+__device__ __forceinline__ uint32_t lsa31(uint32_t y, uint32_t hi, bool asm_form) {
+  if (!asm_form) return (y << 31) + hi;
+  uint32_t r;
+  asm("v_lshl_add_u32 %0, %1, 31, %2" : "=v"(r) : "v"(y), "v"(hi));
   return r;
 }
-__device__ __forceinline__ double logit_resid4(double eta, uint32_t y, const double* tab, double& lm, double& sp) {
+
+template <bool LSA>
+__device__ __forceinline__ double logit_resid4x(double eta, uint32_t y, const double* tab, double& lm, double& sp) {
   constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
   constexpr double INV_L = 1477.3197218702985;            // 1024 / ln 2
   constexpr double L = 0.0006769015435155716;             // ln 2 / 1024
   constexpr double C2 = 0.5000000039583942, C3 = 0.16666666713444417;   // e^r on |r| <= ln2/2048 (fit)
   const uint64_t eb = __builtin_bit_cast(uint64_t, eta);
-  const double s = __builtin_bit_cast(double, (eb & 0xFFFFFFFFull) | ((uint64_t)((y << 31) + (uint32_t)(eb >> 32)) << 32));
+  const double s = __builtin_bit_cast(double, (eb & 0xFFFFFFFFull) | ((uint64_t)lsa31(y, (uint32_t)(eb >> 32), LSA) << 32));
   const double a = fmin_abs(s, 700.0);                    // |s| = |eta|; NaN -> 700 (the NaN stays in lm)
   const double sn = fma(-a, INV_L, MAGIC);
   const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
@@ -95,29 +40,11 @@ __device__ __forceinline__ double logit_resid4(double eta, uint32_t y, const dou
   const uint64_t dvp = __builtin_bit_cast(uint64_t, blend(spos, w, ri));   // dv/sgn
   lm += -s - fabs(s);                                     // t - |t|
   sp = fma(sp, u, e);
-  return __builtin_bit_cast(double, (dvp & 0xFFFFFFFFull) | ((uint64_t)((y << 31) + (uint32_t)(dvp >> 32)) << 32));   // -dv
+  return __builtin_bit_cast(double, (dvp & 0xFFFFFFFFull) | ((uint64_t)lsa31(y, (uint32_t)(dvp >> 32), LSA) << 32));   // -dv
 }
 
-// Geometry of k_sweep16 for a given d (host and device).
-struct S16Geom {
-  int KF, JT, REM, JTM;
-  bool VREM;
-};
-__host__ __device__ constexpr S16Geom s16_geom(int KF) {
-  const int JT = (KF + 3) / 4;                  // 16-column tiles covering 4 KF >= d columns
-  const int REM = 4 * KF - 16 * (JT - 1);       // columns of the last tile (d has up to 3 fewer)
-  const bool VREM = REM <= 4;                   // <= 4: the VALU does the last tile
-  return S16Geom{KF, JT, REM, VREM ? JT - 1 : JT, VREM};
-}
-// d > 108 (KF >= 28): the beta image no longer fits next to the slots at two workgroups per CU,
-// so beta is held in registers, and the backward's A operands (which would not fit in registers
-// beside it) are read from the slot, which is then released after the backward instead of after
-// the forward (the next DMA's latency is covered by the SIMD's other wave only).
-__host__ __device__ constexpr bool s16_breg(int KF) { return KF >= 28; }
-constexpr int S16_FLUSH = 64;                   // sub-tiles between log1p flushes (4 elements each)
-
-template <int FAM, int KF, bool BREG = s16_breg(KF), int NACC = 2>
-__global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
+template <int FAM, int KF, bool BREG = s16_breg(KF), int NACC = 2, bool LSA = false, bool PAIR = false>
+__global__ __launch_bounds__(256, 2) void k_sweep16x(SweepArgs A) {
   constexpr S16Geom g = s16_geom(KF);
   constexpr int C = SM_C, NW = SM_W, JTM = g.JTM, KP = 4 * KF, KB = KP + 2;
   constexpr bool LOGI = FAM == STK_LOGREG;
@@ -201,17 +128,13 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
     ea[0] = dbl4{alpha, alpha, alpha, alpha};
 #pragma unroll
     for (int i = 1; i < NACC; ++i) ea[i] = dbl4{0.0, 0.0, 0.0, 0.0};
-    if (!BREG && (d & 1) == 0) {
-      // even d (16-B aligned rows): k-steps 2m, 2m+1 of lane group lh take columns 8m + 2 lh and
-      // 8m + 2 lh + 1, one ds_read_b128 of X and one of beta per pair instead of two ds_read_b64
-      // each (the beta image is in natural column order either way); KF odd: the last k-step
-      // takes column 8 (KF / 2) + lh.  (A/B at d = 100: 13.88 -> 13.79 ms, profiles/r04c_*)
+    if constexpr (PAIR) {          // k-steps 2m, 2m+1 of lane group lh: columns 8m + 2lh, +1 (one b128 each)
 #pragma unroll
       for (int m = 0; m < KF / 2; ++m) {
-        const dbl2 x2 = *reinterpret_cast<const dbl2*>(xs + lr * d + 8 * m + 2 * lh);
+        const dbl2 xa2 = *reinterpret_cast<const dbl2*>(xs + lr * d + 8 * m + 2 * lh);
         const dbl2 b2 = *reinterpret_cast<const dbl2*>(bimg + lr * KB + 8 * m + 2 * lh);
-        ea[(2 * m) % NACC] = mfma_f64(x2.x, b2.x, ea[(2 * m) % NACC]);
-        ea[(2 * m + 1) % NACC] = mfma_f64(x2.y, b2.y, ea[(2 * m + 1) % NACC]);
+        ea[(2 * m) % NACC] = mfma_f64(xa2.x, b2.x, ea[(2 * m) % NACC]);
+        ea[(2 * m + 1) % NACC] = mfma_f64(xa2.y, b2.y, ea[(2 * m + 1) % NACC]);
       }
       if constexpr (KF & 1) {
         const int col = 8 * (KF / 2) + lh;
@@ -219,10 +142,10 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
       }
     } else {
 #pragma unroll
-      for (int s = 0; s < KF; ++s) {
-        const double b = BREG ? bf[s] : brow[s];
-        ea[s % NACC] = mfma_f64(xrow[std::min(lh * KF + s, d - 1)], b, ea[s % NACC]);
-      }
+    for (int s = 0; s < KF; ++s) {
+      const double b = BREG ? bf[s] : brow[s];
+      ea[s % NACC] = mfma_f64(xrow[std::min(lh * KF + s, d - 1)], b, ea[s % NACC]);
+    }
     }
     // ---- everything else the sub-tile needs from the slot, into registers; then release it
     double xa[4][PRE && JTM > 0 ? JTM : 1];
@@ -261,7 +184,7 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if constexpr (LOGI) {
-          de[i] = logit_resid4(eta4[i], ym[i], tab, lm, sp);
+          de[i] = logit_resid4x<LSA>(eta4[i], ym[i], tab, lm, sp);
         } else {
           const double z = (yv[i] - eta4[i]) * inv_s;
           lm = fma(z, z, lm);
@@ -275,7 +198,7 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
         const bool valid = lh + 4 * i < rv;
         double lm2 = lm, sp2 = sp, dv;
         if constexpr (LOGI) {
-          dv = logit_resid4(eta4[i], ym[i], tab, lm2, sp2);
+          dv = logit_resid4x<LSA>(eta4[i], ym[i], tab, lm2, sp2);
         } else {
           const double z = (yv[i] - eta4[i]) * inv_s;
           lm2 = fma(z, z, lm);
@@ -371,46 +294,5 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
   }
 }
 
+
 }  // namespace stk
-
-using namespace stk;
-
-// LDS bytes of k_sweep16 at d (the main loop's slots + beta image + table + remainder scratch,
-// or the block reduction's area, whichever is larger).
-size_t stk_sweep16_lds_bytes(int family, int d) {
-  const int KF = (d + 3) / 4;
-  const S16Geom g = s16_geom(KF);
-  size_t main = (size_t)SM_W * sweepm_slot_bytes(d) + (s16_breg(KF) ? 0 : (size_t)SM_C * (4 * KF + 2) * 8) +
-                (family == STK_LOGREG ? EX_TAB * 8 : 0) + (size_t)SM_W * 64 * 8;
-  const size_t red = ((size_t)SM_W * g.JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * 8;
-  return std::max(main, red);
-}
-
-template <int FAM, int KF>
-static hipError_t go16(const SweepArgs& A, int nblocks, size_t lds, hipStream_t st) {
-  auto kern = k_sweep16<FAM, KF>;
-  if (const hipError_t e = allow_big_lds((const void*)kern)) return e;
-  hipLaunchKernelGGL(kern, dim3(nblocks), dim3(SM_W * 64), lds, st, A);
-  return hipGetLastError();
-}
-
-template <int FAM>
-static hipError_t launch16(const SweepArgs& A, int d, int nblocks, size_t lds, hipStream_t st) {
-  switch ((d + 3) / 4) {
-#define S16_CASE(K) case K: return go16<FAM, K>(A, nblocks, lds, st);
-    S16_CASE(1) S16_CASE(2) S16_CASE(3) S16_CASE(4) S16_CASE(5) S16_CASE(6) S16_CASE(7) S16_CASE(8)
-    S16_CASE(9) S16_CASE(10) S16_CASE(11) S16_CASE(12) S16_CASE(13) S16_CASE(14) S16_CASE(15) S16_CASE(16)
-    S16_CASE(17) S16_CASE(18) S16_CASE(19) S16_CASE(20) S16_CASE(21) S16_CASE(22) S16_CASE(23) S16_CASE(24)
-    S16_CASE(25) S16_CASE(26) S16_CASE(27) S16_CASE(28) S16_CASE(29) S16_CASE(30) S16_CASE(31) S16_CASE(32)
-#undef S16_CASE
-  }
-  return hipErrorInvalidValue;
-}
-
-bool stk_sweep16_supported(int d) { return d >= 1 && d <= 128; }
-
-hipError_t stk_launch_sweep16(int family, const SweepArgs& A, int d, int nblocks, size_t lds, hipStream_t st) {
-  if (family == STK_LOGREG) return launch16<STK_LOGREG>(A, d, nblocks, lds, st);
-  if (family == STK_LINREG) return launch16<STK_LINREG>(A, d, nblocks, lds, st);
-  return hipErrorInvalidValue;
-}
