@@ -186,8 +186,11 @@ def select_pars(family: str, data: dict, pars=None, include: bool = True) -> "li
     """pystan 2 ``sampling(pars=..., include=...)`` (forwarded by stark/stark.py:48 **kwargs):
     the rows that ``fit.extract()`` then returns, in its key order.  pars names the parameters
     to keep (include=True, in the given order) or to drop (include=False, model order kept);
-    lp__ is always returned, last.  Unknown names raise ValueError as pystan does.  None: all
-    rows (no selection)."""
+    lp__ is always returned, last, once (an explicit 'lp__' in pars is that same row).  Unknown
+    names raise ValueError as pystan does.  None: all rows (no selection).
+    Parity UNPINNED against pystan itself: pystan is not importable here, and the golden fixture
+    (tests/golden/make_golden.py, FakeStanModel) encodes this same reading of pystan 2's
+    extract() order, so the driver test pins the reshape, not the selection order."""
     if pars is None:
         return None
     if isinstance(pars, str):

@@ -37,6 +37,7 @@ struct Arm {
   const void* kern;
   size_t lds;
   std::vector<float> ms;
+  int G = 0;                // chunks per shard (0: the library's geometry)
 };
 
 int main(int argc, char** argv) {
@@ -84,7 +85,7 @@ int main(int argc, char** argv) {
   int T, LD, G;
   size_t lds;
   stk_sweep_geometry(rows, d, &T, &LD, &G, &lds, C);
-  CK(hipMalloc(&partial, sizeof(double) * (size_t)nsh * G * C * (d + 2)));
+  CK(hipMalloc(&partial, sizeof(double) * (size_t)nsh * 2048 * C * (d + 2)));   // room for G <= 2048
   CK(hipMalloc(&lp, sizeof(double) * nsh * C));
   CK(hipMalloc(&grad, sizeof(double) * nsh * C * Dp));
   CK(hipStreamSynchronize(st));
@@ -100,12 +101,9 @@ int main(int argc, char** argv) {
 #define ARMS(F, KF, JT)                                                                        \
   arms = {{"s16", (const void*)k_sweep16<F, KF>, l16, {}},                                     \
           {"e3", (const void*)k_sweepe<F, KF, JT, 0, 3, 2, 0, 2, 1>, lds, {}},                 \
-          {"x-lsa", (const void*)k_sweep16x<F, KF, false, 2, true, false>, l16, {}},           \
-          {"x-lsa-n1", (const void*)k_sweep16x<F, KF, false, 1, true, false>, l16, {}},        \
-          {"x-pair", (const void*)k_sweep16x<F, KF, false, 2, false, true>, l16, {}},          \
-          {"x-lsa-pair", (const void*)k_sweep16x<F, KF, false, 2, true, true>, l16, {}},       \
-          {"x-breg", (const void*)k_sweep16x<F, KF, true, 2, false, false>, l16, {}},          \
-          {"x-breg-lsa", (const void*)k_sweep16x<F, KF, true, 2, true, false>, l16, {}}};
+          {"s16-g1024", (const void*)k_sweep16<F, KF>, l16, {}, 1024},                         \
+          {"s16-g2048", (const void*)k_sweep16<F, KF>, l16, {}, 2048},                         \
+          {"s16-g768", (const void*)k_sweep16<F, KF>, l16, {}, 768}};
   if (fam == STK_LOGREG) {
     if (d == 100) { ARMS(STK_LOGREG, 25, 7) } else { ARMS(STK_LOGREG, 13, 4) }
   } else {
@@ -113,14 +111,17 @@ int main(int argc, char** argv) {
   }
   for (auto& a : arms) CK(hipFuncSetAttribute(a.kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   auto launch = [&](const Arm& a) {
-    hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.kern)), dim3(nsh * G), dim3(256), a.lds,
-                       st, A);
+    SweepArgs B = A;
+    B.G = B.Gs = a.G ? a.G : G;
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.kern)), dim3(nsh * B.G), dim3(256),
+                       a.lds, st, B);
   };
   std::vector<std::vector<double>> res;
   for (size_t k = 0; k < arms.size(); ++k) {
     launch(arms[k]);
     CK(hipGetLastError());
-    CK(stk_launch_sweep_reduce(fam, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
+    const int Gk = arms[k].G ? arms[k].G : G;
+    CK(stk_launch_sweep_reduce(fam, sh_d, 0, nsh, d, Gk, Gk, q, C, Dp, partial, nullptr, 0, lp, grad, st));
     std::vector<double> h((size_t)nsh * C * (Dp + 1));
     CK(hipMemcpyAsync(h.data(), lp, sizeof(double) * nsh * C, hipMemcpyDeviceToHost, st));
     CK(hipMemcpyAsync(h.data() + nsh * C, grad, sizeof(double) * nsh * C * Dp, hipMemcpyDeviceToHost, st));
