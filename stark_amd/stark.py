@@ -112,6 +112,16 @@ def _unconstrain(family, data, init_dict):
     return np.asarray(v)
 
 
+def thin_draws(draws, chains, thin):
+    """Stan's num_thin: of each chain's post-warmup iterations m = 0, 1, ... keep those with
+    m % thin == 0 (ceil(S / thin) draws per chain; services/util/generate_transitions), columns
+    chain-major as the sampler writes them."""
+    if thin == 1:
+        return draws
+    P, n = draws.shape
+    return np.ascontiguousarray(draws.reshape(P, chains, n // chains)[:, :, ::thin].reshape(P, -1))
+
+
 def sampling_config(family, datas, **kw):
     """pystan 2 ``StanModel.sampling`` keywords -> engine config (stark/stark.py:48)."""
     kw = dict(kw)
@@ -120,15 +130,15 @@ def sampling_config(family, datas, **kw):
     chains = int(kw.pop("chains", 4))
     kw.pop("n_jobs", None)
     thin = int(kw.pop("thin", 1))
-    if thin != 1:
-        raise NotImplementedError("thin != 1 is not supported")
+    if thin < 1:
+        raise ValueError("thin must be a positive integer")
     seed = kw.pop("seed", None)
     if seed is None:
         seed = int(np.random.SeedSequence().entropy) & 0x7FFFFFFF
     control = dict(kw.pop("control", None) or {})
     if control.pop("metric", "diag_e") != "diag_e":
         raise NotImplementedError("only metric='diag_e' (Stan's default) is supported")
-    cfg = dict(num_warmup=warmup, num_samples=it - warmup, chains=chains, seed=seed)
+    cfg = dict(num_warmup=warmup, num_samples=it - warmup, chains=chains, seed=seed, thin=thin)
     for k, v in control.items():
         if k not in _CONTROL_KEYS:
             raise ValueError(f"unknown control key {k!r}")
@@ -143,6 +153,13 @@ def sampling_config(family, datas, **kw):
     if init == "0":
         D = [len(_unconstrain(family, d, {})) for d in datas]
         cfg["init"] = np.concatenate([np.zeros(Ds * chains) for Ds in D])
+    elif callable(init):
+        # pystan 2: init(chain_id=...) per chain, or init() when it takes no chain_id
+        try:
+            dicts = [init(chain_id=c) for c in range(chains)]
+        except TypeError:
+            dicts = [init() for _ in range(chains)]
+        cfg["init"] = np.concatenate([_unconstrain(family, d, dicts[c]) for d in datas for c in range(chains)])
     elif isinstance(init, (list, tuple)):
         if len(init) != chains:
             raise ValueError("init list must have one dict per chain")
@@ -204,6 +221,7 @@ class Stark:
         cfg = sampling_config(self.family, datas, **kwargs)
         if shard_ids is not None:
             cfg["shard_ids"] = shard_ids
+        thin = cfg.pop("thin", 1)
         model = engine.Model(engine.default_context(), self.family, shards)
         if getattr(self, "priors", None):
             model.set_prior(**self.priors)
@@ -212,10 +230,11 @@ class Stark:
         finally:
             model.close()
         self.last_run = res
+        draws = [thin_draws(d, cfg["chains"], thin) for d in res.draws]
         if not permuted:
-            return res.draws
+            return draws
         ids = shard_ids if shard_ids is not None else range(len(datas))
-        return [permute_draws(d, cfg["chains"], cfg["seed"], p) for d, p in zip(res.draws, ids)]
+        return [permute_draws(d, cfg["chains"], cfg["seed"], p) for d, p in zip(draws, ids)]
 
     def _mcmc(self, callback, **kwargs):
         def w(sts):

@@ -101,10 +101,28 @@ def test_sampling_config_mapping():
     assert c0["init"].shape == (12,) and not c0["init"].any()
     ci = sampling_config("schools", datas, iter=20, chains=1, seed=1, init=[{"mu": 1.0, "tau": np.e}])
     assert ci["init"][0] == 1.0 and abs(ci["init"][1] - 1.0) < 1e-15
-    with pytest.raises(NotImplementedError):
-        sampling_config("schools", datas, thin=2)
+    with pytest.raises(ValueError):
+        sampling_config("schools", datas, thin=0)
+    assert sampling_config("schools", datas, iter=20, thin=3, seed=1)["thin"] == 3
+    # callable init, pystan 2: init(chain_id=c), or init() when it takes no chain_id
+    cf = sampling_config("schools", datas, iter=20, chains=2, seed=1, init=lambda chain_id: {"mu": chain_id + 0.5})
+    assert cf["init"][0] == 0.5 and cf["init"][6] == 1.5
+    cg = sampling_config("schools", datas, iter=20, chains=2, seed=1, init=lambda: {"tau": 2.0})
+    assert abs(cg["init"][1] - np.log(2.0)) < 1e-15 and abs(cg["init"][7] - np.log(2.0)) < 1e-15
     with pytest.raises(TypeError):
         sampling_config("schools", datas, bogus=1)
+
+
+def test_thin_draws_keeps_every_thin_th_iteration_per_chain():
+    """Stan's num_thin (services/util/generate_transitions: save when m % num_thin == 0):
+    ceil(S / thin) draws per chain, chain-major columns as the sampler writes them."""
+    from stark_amd.stark import thin_draws
+    P, chains, S = 3, 2, 7
+    d = np.arange(P * chains * S, dtype=float).reshape(P, chains * S)
+    t = thin_draws(d, chains, 3)
+    assert t.shape == (P, chains * 3)
+    np.testing.assert_array_equal(t[0], [0, 3, 6, 7, 10, 13])
+    assert thin_draws(d, chains, 1) is d
 
 
 # ---------------------------------------------------------------- RDD shim
