@@ -155,10 +155,11 @@ __device__ __forceinline__ double log1p01_mt(double e, const double* t) {   // e
   return fma(rl, q, cj[2]);
 }
 __device__ __forceinline__ double log_sum_exp_mt(double a, double b, const double* t) {   // as log_sum_exp2
-  if (a == -INFINITY) return b;
-  if (a == INFINITY && b == INFINITY) return INFINITY;
-  if (a > b) return a + log1p01_mt(exp_mt(b - a, t), t);
-  return b + log1p01_mt(exp_mt(a - b, t), t);
+  // branch-free: max + log1p(exp(-|a - b|)), with log_sum_exp2's two special cases as selects
+  // (a = -inf with b finite needs none: exp(-inf) = 0 gives b)
+  const double r = fmax(a, b) + log1p01_mt(exp_mt(-fabs(a - b), t), t);
+  const double r1 = (a == INFINITY && b == INFINITY) ? INFINITY : r;
+  return a == -INFINITY ? b : r1;
 }
 
 // ------------------------------------------------------------------ model hooks
@@ -403,7 +404,33 @@ struct NutsChain {
   // uniforms k = 2m and 2m + 1 of a transition come from one Philox block: the odd one is kept
   // from the even one's call (u_key = the block's (iteration, m) + 1; 0 = nothing kept)
   uint64_t u_odd = 0, u_key = 0;
+  // FM (the fused kernel): the transition's uniforms come from a window of 2 SEG precomputed in
+  // the chain's LDS slots ub[] -- lane l of the chain computes Philox block base/2 + l, so a
+  // window costs ONE Philox latency for all its 2 SEG uniforms -- and uniform() is a branch-free
+  // LDS read: the sub-tree merge loop is then one basic block whose chains (the stack loads and
+  // U-turn sums, the log_sum_exp / exp, the uniform) the compiler can interleave.  Same counter
+  // mapping as the direct form (uniform k = element k & 1 of block k >> 1): identical draws.
+  double* ub = nullptr;
+  int ub_base = 0;
+  __device__ __forceinline__ void fill_uniforms(int base) {   // window [base, base + 2 SEG), base even
+    const uint32_t it = (uint32_t)(IV(I_ITER) + A.iter_offset);
+    const u64x2 r = philox(A.seed, rid, it, (uint32_t)(base >> 1) + (uint32_t)lane, TAG_UNI);
+    const dbl2 v = {u53(r.a), u53(r.b)};
+    *reinterpret_cast<dbl2*>(ub + 2 * lane) = v;
+    ub_base = base;
+  }
+  // a step takes at most max_depth + 1 uniforms (merges, the top level, the next sub-tree's direction)
+  __device__ __forceinline__ void ensure_uniforms() {
+    if constexpr (FM) {
+      const int k = IV(I_UK);
+      if (k - ub_base + A.max_depth + 2 > 2 * SEG) fill_uniforms(k & ~1);
+    }
+  }
   __device__ __forceinline__ double uniform() {
+    if constexpr (FM) {
+      const int k = IV(I_UK)++;
+      return ub[k - ub_base];
+    }
     const uint32_t it = (uint32_t)(IV(I_ITER) + A.iter_offset);
     const uint32_t k = (uint32_t)IV(I_UK)++;
     const uint64_t key = (((uint64_t)it << 32) | (k >> 1)) + 1;
@@ -536,6 +563,7 @@ struct NutsChain {
     if (A.jitter > 0)
       S(S_EPS) *= 1.0 + A.jitter * (2.0 * uniform_at(A.seed, rid, (uint32_t)(IV(I_ITER) + A.iter_offset), 0u, TAG_JIT) - 1.0);
     IV(I_UK) = 0;
+    if constexpr (FM) fill_uniforms(0);
     load_sample_point();
     sample_momentum((uint32_t)(IV(I_ITER) + A.iter_offset), 0u, TAG_MOM);
     const double H0 = S(S_V) + kinetic(p);
@@ -687,7 +715,19 @@ struct NutsChain {
       const double lsw_sub = lse(l_lsw, c_lsw);
       const double u = uniform();
       const bool take_right = (c_lsw > lsw_sub) || (u < ex(c_lsw - lsw_sub));
-      if (!take_right) {
+      if constexpr (FM) {   // the left sub-tree's sample read unconditionally and selected: no branch
+        double l_q[NCH], l_g[NCH];
+        ld(svp(j, SV_Q), l_q);
+        ld(svp(j, SV_G), l_g);
+        const double l_V = stks[j * SS_COUNT + SS_V], l_H = stks[j * SS_COUNT + SS_H];
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+          c_q[k] = take_right ? c_q[k] : l_q[k];
+          c_g[k] = take_right ? c_g[k] : l_g[k];
+        }
+        c_V = take_right ? c_V : l_V;
+        c_H = take_right ? c_H : l_H;
+      } else if (!take_right) {
         ld(svp(j, SV_Q), c_q);
         ld(svp(j, SV_G), c_g);
         c_V = stks[j * SS_COUNT + SS_V];
@@ -907,7 +947,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   const size_t nv = (size_t)V_COUNT * A.Dp, ns = (size_t)A.max_depth * stack_vecs(A) * A.Dp;
   const size_t nss = (size_t)A.max_depth * SS_COUNT;
   constexpr size_t nsc = S_COUNT + (I_COUNT + 1) / 2;   // the chain's scalars and counters
-  const size_t per = (nv + ns + nss + nsc + 1) & ~(size_t)1;      // per-chain image, even (table 16-B aligned)
+  const size_t per = (nv + ns + nss + nsc + 2 * SEG + 1) & ~(size_t)1;   // per-chain image + uniform window, even
   double* const fl = fl_all + (size_t)seg * per;
   double* const mtab = fl_all + (size_t)CPW * per;                   // exp / log1p table (MT_N doubles)
   mt_init(mtab, (int)threadIdx.x, WAVE);
@@ -932,7 +972,9 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   if (run) {
     NutsChain<NCH, SEG, true> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
     ch.mt = mtab;
+    ch.ub = fl + ((nv + ns + nss + nsc + 1) & ~(size_t)1);   // after the chain's image, 16-B aligned: 2 SEG doubles
     ch.load();
+    ch.fill_uniforms(ch.IV(I_UK) & ~1);                // the current transition's window (a resumed chain)
     double yc[NCH], isc[NCH];
     schools_data<NCH, SEG>(ch.sh, yc, isc, lane, ch.D);
     const int mode = ch.IV(I_MODE);
@@ -953,6 +995,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
       unsigned long long ngrad = 0;
       while (req && steps < max_steps) {
         double glp[NCH];
+        ch.ensure_uniforms();
         const double lp = schools_lpgrad<NCH, SEG, true>(yc, isc, ch.q, glp, lane, ch.D, mtab);
         ++steps;
         req = ch.consume(lp, glp, pause_at);
@@ -1013,8 +1056,9 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
 }
 template <int NCH, int CPW, int MINW = 1>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
+  constexpr int SEG = WAVE / CPW;
   size_t per = (size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp + (size_t)A.max_depth * SS_COUNT +
-               S_COUNT + (I_COUNT + 1) / 2;
+               S_COUNT + (I_COUNT + 1) / 2 + 2 * SEG;  // + the chain's uniform window
   per += per & 1;                                        // keep the table after the chains 16-B aligned
   const size_t lds = sizeof(double) * (CPW * per + MT_N);
   if (lds > 64 * 1024) {
