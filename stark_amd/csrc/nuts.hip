@@ -334,7 +334,22 @@ struct NutsChain {
   __device__ __forceinline__ double* svp(int level, int v) const {
     return stk + ((size_t)level * stack_vecs(A) + v) * A.Dp;
   }
+  // FM (the fused kernel, where every vector lives in the workgroup's LDS image): the load is
+  // unconditional and lanes past D select 0 -- an exec-masked load would split the basic block
+  // (s_cbranch_execz) and keep the compiler from interleaving a merge's independent chains.  Lanes
+  // past D read inside the image (the next vector, the stack scalars, the next chain or the table).
   __device__ __forceinline__ void ld(const double* base, double (&r)[NCH]) const {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      if constexpr (FM) {
+        const double v = base[k * SEG + lane];
+        r[k] = ok(k) ? v : 0.0;
+      } else {
+        r[k] = ok(k) ? base[k * SEG + lane] : 0.0;
+      }
+    }
+  }
+  __device__ __forceinline__ void ldg(const double* base, double (&r)[NCH]) const {   // global memory: masked
 #pragma unroll
     for (int k = 0; k < NCH; ++k) r[k] = ok(k) ? base[k * SEG + lane] : 0.0;
   }
@@ -987,7 +1002,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
         if (req && lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += 1;
       }
     } else {
-      ch.ld(A.qeval + (size_t)gid * A.Dp, ch.q);   // the pending request
+      ch.ldg(A.qeval + (size_t)gid * A.Dp, ch.q);  // the pending request
       req = true;
     }
     if (go) {
