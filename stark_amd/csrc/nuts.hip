@@ -268,7 +268,9 @@ __device__ __forceinline__ void write_draw(const NutsArgs& A, const ShardDev& sh
 // ------------------------------------------------------------------ the chain
 // SEG: lanes per chain (64: one chain per wave; 16 / 32: 4 / 2 chains packed in a wave, each
 // in its own DPP row(s), D <= SEG).  `lane` is the lane's position inside its segment.
-template <int NCH, int SEG = WAVE, bool FM = false>
+template <int NCH, int SEG = WAVE, bool FM = false, int UT = -1>
+// UT: the U-turn criterion at compile time (0: Stan 2.19, 1: Stan >= 2.23's junction checks; -1: at
+// run time from A.uturn_ext) -- a run-time branch on it splits the merge loop's basic block
 // (every member is force-inlined: a non-inlined constructor or method receiving `this` puts
 // the whole chain object -- s[], iv[], q, p, g -- in scratch memory; 48.7 -> 26.1 us per step,
 // profiles/r02q_kernel_stats.csv vs r02r_kernel_stats_global.csv)
@@ -329,10 +331,14 @@ struct NutsChain {
   __device__ __forceinline__ double& S(int i) { return cold_s(i) ? scold[i] : s[i]; }
   __device__ __forceinline__ int& IV(int i) { return cold_i(i) ? icold[i] : iv[i]; }
 
+  __device__ __forceinline__ bool uext() const {
+    if constexpr (UT >= 0) return UT != 0;
+    else return A.uturn_ext != 0;
+  }
   __device__ __forceinline__ bool ok(int k) const { return k * SEG + lane < D; }
   __device__ __forceinline__ double* vp(int v) const { return vec + (size_t)v * A.Dp; }
   __device__ __forceinline__ double* svp(int level, int v) const {
-    return stk + ((size_t)level * stack_vecs(A) + v) * A.Dp;
+    return stk + ((size_t)level * (uext() ? SV_COUNT : SV_PB) + v) * A.Dp;   // stack_vecs(A)
   }
   // FM (the fused kernel, where every vector lives in the workgroup's LDS image): the load is
   // unconditional and lanes past D select 0 -- an exec-masked load would split the basic block
@@ -749,7 +755,7 @@ struct NutsChain {
         c_H = stks[j * SS_COUNT + SS_H];
       }
       bool junction_ok = true;
-      if (A.uturn_ext) {
+      if (uext()) {
         // Stan >= 2.23: the left half extended by the right half's first momentum, and the
         // right half extended by the left half's last momentum, must not turn either
         double l_pb[NCH], l_pe[NCH], l_pse[NCH], e1[NCH], e2[NCH];
@@ -782,7 +788,7 @@ struct NutsChain {
       st(svp(j, SV_PSB), c_psb);
       st(svp(j, SV_Q), c_q);
       st(svp(j, SV_G), c_g);
-      if (A.uturn_ext) {
+      if (uext()) {
         st(svp(j, SV_PB), c_pb);
         st(svp(j, SV_PE), p);          // its last leaf is the latest one
         st(svp(j, SV_PSE), c_pse);
@@ -797,33 +803,60 @@ struct NutsChain {
     // the top-level sub-tree of this depth is complete and valid
     const int fwd = IV(I_DIR) > 0;
     double o_p[NCH], o_ps[NCH];     // the old trajectory's end next to the new sub-tree
-    if (A.uturn_ext) {
+    if (uext()) {
       ld(vp(fwd ? V_PF : V_PB), o_p);
       ld(vp(fwd ? V_PSP : V_PSM), o_ps);
     }
     st(vp(fwd ? V_QF : V_QB), q);
     st(vp(fwd ? V_PF : V_PB), p);
     st(vp(fwd ? V_GF : V_GB), g);
-    if (fwd) S(S_VF) = S(S_V);            // (no run-time index into the register arrays: that
-    else S(S_VB) = S(S_V);                //  would move them to scratch)
+    // (no run-time index into the register arrays: that would move them to scratch)
+    S(S_VF) = fwd ? S(S_V) : S(S_VF);
+    S(S_VB) = fwd ? S(S_VB) : S(S_V);
     IV(I_DEPTH) = depth + 1;
     const double u = uniform();
-    if (c_lsw > S(S_LSW) || u < ex(c_lsw - S(S_LSW))) {
-      st(vp(V_QS), c_q);
-      st(vp(V_GS), c_g);
-      S(S_VS) = c_V;
-      S(S_HS) = c_H;
+    const bool take = c_lsw > S(S_LSW) || u < ex(c_lsw - S(S_LSW));
+    double rho[NCH], psp[NCH], psm[NCH], rho_old[NCH];
+    if constexpr (FM) {   // branch-free: the sample point rewritten with a select (LDS image)
+      double o_q[NCH], o_g[NCH], nq[NCH], ng[NCH];
+      ld(vp(V_QS), o_q);
+      ld(vp(V_GS), o_g);
+      ld(vp(V_RHO), rho);
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        nq[k] = take ? c_q[k] : o_q[k];
+        ng[k] = take ? c_g[k] : o_g[k];
+      }
+      st(vp(V_QS), nq);
+      st(vp(V_GS), ng);
+      S(S_VS) = take ? c_V : S(S_VS);
+      S(S_HS) = take ? c_H : S(S_HS);
+    } else {
+      if (take) {
+        st(vp(V_QS), c_q);
+        st(vp(V_GS), c_g);
+        S(S_VS) = c_V;
+        S(S_HS) = c_H;
+      }
+      ld(vp(V_RHO), rho);
     }
     S(S_LSW) = lse(S(S_LSW), c_lsw);
-    double rho[NCH], psp[NCH], psm[NCH], rho_old[NCH];
-    ld(vp(V_RHO), rho);
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       rho_old[k] = rho[k];
       rho[k] = rho[k] + c_rho[k];
     }
     st(vp(V_RHO), rho);
-    if (fwd) {
+    if constexpr (FM) {   // the end this sub-tree extends gets its p_sharp; the other end's is read
+      double oth[NCH];
+      st(vp(fwd ? V_PSP : V_PSM), c_pse);
+      ld(vp(fwd ? V_PSM : V_PSP), oth);
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        psp[k] = fwd ? c_pse[k] : oth[k];
+        psm[k] = fwd ? oth[k] : c_pse[k];
+      }
+    } else if (fwd) {
       st(vp(V_PSP), c_pse);
 #pragma unroll
       for (int k = 0; k < NCH; ++k) psp[k] = c_pse[k];
@@ -835,7 +868,7 @@ struct NutsChain {
       ld(vp(V_PSP), psp);
     }
     bool junction_ok = true;
-    if (A.uturn_ext) {
+    if (uext()) {
       // the new sub-tree against the old trajectory across their junction (base_nuts::transition)
       double e1[NCH], e2[NCH];
 #pragma unroll
@@ -951,7 +984,7 @@ __global__ __launch_bounds__(64) void k_nuts_step(NutsArgs A, int step_id, int p
 // chain per wave leaves 54 of 64 lanes idle, four per wave leave 24.  Every chain still runs
 // its own state machine; lanes of one chain always take the same branch, and the segmented
 // sums stay inside a chain's DPP row(s), so chains in other states never interfere.
-template <int NCH, int CPW, int MINW = 1>
+template <int NCH, int CPW, int MINW = 1, int UT = 0>
 __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int pause_at, int max_steps) {
   constexpr int SEG = WAVE / CPW;
   static_assert(CPW == 1 || NCH == 1, "packed chains hold one chunk of lanes each");
@@ -985,7 +1018,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   }
   __syncthreads();
   if (run) {
-    NutsChain<NCH, SEG, true> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
+    NutsChain<NCH, SEG, true, UT> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
     ch.mt = mtab;
     ch.ub = fl + ((nv + ns + nss + nsc + 1) & ~(size_t)1);   // after the chain's image, 16-B aligned: 2 SEG doubles
     ch.load();
@@ -1069,8 +1102,8 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
   hipLaunchKernelGGL(k_nuts_step<NCH>, dim3(A.nchains), dim3(64), 0, st, A, step_id, pause_at);
   return hipGetLastError();
 }
-template <int NCH, int CPW, int MINW = 1>
-static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
+template <int NCH, int CPW, int MINW = 1, int UT = 0>
+static hipError_t launch_fused_ut(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
   constexpr int SEG = WAVE / CPW;
   size_t per = (size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp + (size_t)A.max_depth * SS_COUNT +
                S_COUNT + (I_COUNT + 1) / 2 + 2 * SEG;  // + the chain's uniform window
@@ -1079,11 +1112,16 @@ static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps,
   if (lds > 64 * 1024) {
     // the attribute is per device (allow_big_lds keys it on the current one); a failure is
     // reported as such rather than as a generic launch failure
-    if (const hipError_t e = allow_big_lds((const void*)k_nuts_fused_schools<NCH, CPW, MINW>)) return e;
+    if (const hipError_t e = allow_big_lds((const void*)k_nuts_fused_schools<NCH, CPW, MINW, UT>)) return e;
   }
-  hipLaunchKernelGGL((k_nuts_fused_schools<NCH, CPW, MINW>), dim3((A.nchains + CPW - 1) / CPW), dim3(64), lds, st, A,
-                     pause_at, max_steps);
+  hipLaunchKernelGGL((k_nuts_fused_schools<NCH, CPW, MINW, UT>), dim3((A.nchains + CPW - 1) / CPW), dim3(64), lds, st,
+                     A, pause_at, max_steps);
   return hipGetLastError();
+}
+template <int NCH, int CPW, int MINW = 1>
+static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
+  return A.uturn_ext ? launch_fused_ut<NCH, CPW, MINW, 1>(A, pause_at, max_steps, st)
+                     : launch_fused_ut<NCH, CPW, MINW, 0>(A, pause_at, max_steps, st);
 }
 
 // chains per wave of the fused 8-schools kernel: 4 for D <= 16, 2 for D <= 32, capped by the
