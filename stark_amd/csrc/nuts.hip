@@ -154,6 +154,14 @@ __device__ __forceinline__ double log1p01_mt(double e, const double* t) {   // e
   const double q = fma(fma(fma(fma(fma(fma(1.0 / 7.0, rl, -1.0 / 6.0), rl, 0.2), rl, -0.25), rl, 1.0 / 3.0), rl, -0.5), rl, 1.0);
   return fma(rl, q, cj[2]);
 }
+// log_sum_exp_mt that also returns e = exp(-|a - b|), from which the merge's and the top level's
+// acceptance probabilities follow without a second exp (see NutsChain::on_leaf)
+__device__ __forceinline__ double log_sum_exp_mt_e(double a, double b, const double* t, double& e) {
+  e = exp_mt(-fabs(a - b), t);
+  const double r = fmax(a, b) + log1p01_mt(e, t);
+  const double r1 = (a == INFINITY && b == INFINITY) ? INFINITY : r;
+  return a == -INFINITY ? b : r1;
+}
 __device__ __forceinline__ double log_sum_exp_mt(double a, double b, const double* t) {   // as log_sum_exp2
   // branch-free: max + log1p(exp(-|a - b|)), with log_sum_exp2's two special cases as selects
   // (a = -inf with b finite needs none: exp(-inf) = 0 gives b)
@@ -733,9 +741,20 @@ struct NutsChain {
       double l_rho[NCH], l_psb[NCH];
       ld(svp(j, SV_RHO), l_rho);
       ld(svp(j, SV_PSB), l_psb);
-      const double lsw_sub = lse(l_lsw, c_lsw);
+      double lsw_sub;
+      bool take_right;
       const double u = uniform();
-      const bool take_right = (c_lsw > lsw_sub) || (u < ex(c_lsw - lsw_sub));
+      if constexpr (FM) {
+        // exp(c_lsw - lsw_sub) = 1 / (1 + exp(l_lsw - c_lsw)): with e = exp(-|l_lsw - c_lsw|) from
+        // the log_sum_exp, u < 1/(1 + e) (c >= l) or e/(1 + e) (c < l), compared without a division
+        // (c_lsw > lsw_sub never holds); the same decision up to the last bits of the probability
+        double e;
+        lsw_sub = log_sum_exp_mt_e(l_lsw, c_lsw, mt, e);
+        take_right = u * (1.0 + e) < (c_lsw >= l_lsw ? 1.0 : e);
+      } else {
+        lsw_sub = lse(l_lsw, c_lsw);
+        take_right = (c_lsw > lsw_sub) || (u < ex(c_lsw - lsw_sub));
+      }
       if constexpr (FM) {   // the left sub-tree's sample read unconditionally and selected: no branch
         double l_q[NCH], l_g[NCH];
         ld(svp(j, SV_Q), l_q);
@@ -815,7 +834,16 @@ struct NutsChain {
     S(S_VB) = fwd ? S(S_VB) : S(S_V);
     IV(I_DEPTH) = depth + 1;
     const double u = uniform();
-    const bool take = c_lsw > S(S_LSW) || u < ex(c_lsw - S(S_LSW));
+    bool take;
+    double lsw_new;
+    if constexpr (FM) {   // one exp for both: e = exp(-|c_lsw - lsw|) is exp(c_lsw - lsw) when c_lsw <= lsw
+      double e;
+      lsw_new = log_sum_exp_mt_e(S(S_LSW), c_lsw, mt, e);
+      take = c_lsw > S(S_LSW) || u < e;
+    } else {
+      take = c_lsw > S(S_LSW) || u < ex(c_lsw - S(S_LSW));
+      lsw_new = lse(S(S_LSW), c_lsw);
+    }
     double rho[NCH], psp[NCH], psm[NCH], rho_old[NCH];
     if constexpr (FM) {   // branch-free: the sample point rewritten with a select (LDS image)
       double o_q[NCH], o_g[NCH], nq[NCH], ng[NCH];
@@ -840,7 +868,7 @@ struct NutsChain {
       }
       ld(vp(V_RHO), rho);
     }
-    S(S_LSW) = lse(S(S_LSW), c_lsw);
+    S(S_LSW) = lsw_new;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       rho_old[k] = rho[k];

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 4, call k: fused 8-schools kernel with one exp shared by log_sum_exp and the acceptance tests (new) against the
+# previous commit (base), alternating; NUTS tests first; then the stamped breakdown.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r04k
+mkdir -p $O
+timeout -k 10 400 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_nuts.py tests/test_gpu_consensus.py > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit 4
+for v in base new base2 new2 base3 new3; do
+  case $v in base*) L=$GRAFT_REPO_ROOT/tools/_bin/base_lib/libstark_hip.so;; *) L=$GRAFT_REPO_ROOT/stark_amd/_lib/libstark_hip.so;; esac
+  STARK_HIP_LIB=$L timeout -k 10 120 python3 -u tools/bench_schools.py > $O/schools_$v.json 2> $O/schools_$v.err || exit 5
+  python3 -c "import json; d=json.load(open('$O/schools_$v.json')); print('$v', round(d['value']/1e6,1), 'M grads/s', round(d['ess_per_sec_sampling']/1e6,2), 'M ESS/s', d['leapfrogs_per_transition'], d['posterior_mean_mu_tau'])"
+done
+timeout -k 10 120 python3 -u tools/schools_stamps.py run > $O/stamps.json 2> $O/stamps.err
+echo "stamps rc=$?"; cat $O/stamps.json
