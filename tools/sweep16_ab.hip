@@ -101,9 +101,10 @@ int main(int argc, char** argv) {
 #define ARMS(F, KF, JT)                                                                        \
   arms = {{"s16", (const void*)k_sweep16<F, KF>, l16, {}},                                     \
           {"e3", (const void*)k_sweepe<F, KF, JT, 0, 3, 2, 0, 2, 1>, lds, {}},                 \
-          {"s16-g1024", (const void*)k_sweep16<F, KF>, l16, {}, 1024},                         \
-          {"s16-g2048", (const void*)k_sweep16<F, KF>, l16, {}, 2048},                         \
-          {"s16-g768", (const void*)k_sweep16<F, KF>, l16, {}, 768}};
+          {"x-pair", (const void*)k_sweep16x<F, KF, false, 2, false, true, 0>, l16, {}},       \
+          {"x-pb1", (const void*)k_sweep16x<F, KF, false, 2, false, true, 1>, l16, {}},        \
+          {"x-pb2", (const void*)k_sweep16x<F, KF, false, 2, false, true, 2>, l16, {}},        \
+          {"x-pb3", (const void*)k_sweep16x<F, KF, false, 2, false, true, 3>, l16, {}}};
   if (fam == STK_LOGREG) {
     if (d == 100) { ARMS(STK_LOGREG, 25, 7) } else { ARMS(STK_LOGREG, 13, 4) }
   } else {

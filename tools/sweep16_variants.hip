@@ -3,6 +3,8 @@
 //   BREG / NACC   as the product (beta in registers + late slot release; forward accumulators)
 //   LSA           (y << 31) + hi as ONE v_lshl_add_u32 per use (inline asm; the compiler otherwise
 //                 shares one v_lshlrev_b32 between the two uses and adds twice: 3 instructions)
+//   PB            wave priority: 0 the product (2 over the residual), 1 + a static 1 for odd blocks
+//                 (the SIMD partner that loses arbitration), 2 none at all, 3 the static one only
 //   PAIR          the forward's k-steps 2m, 2m+1 read columns 8m + 2 lh, +1 of X and beta as one
 //                 ds_read_b128 each (needs an even d), instead of two ds_read_b64
 // Included after sweep16.hip (namespace stk).
@@ -43,7 +45,7 @@ __device__ __forceinline__ double logit_resid4x(double eta, uint32_t y, const do
   return __builtin_bit_cast(double, (dvp & 0xFFFFFFFFull) | ((uint64_t)lsa31(y, (uint32_t)(dvp >> 32), LSA) << 32));   // -dv
 }
 
-template <int FAM, int KF, bool BREG = s16_breg(KF), int NACC = 2, bool LSA = false, bool PAIR = false>
+template <int FAM, int KF, bool BREG = s16_breg(KF), int NACC = 2, bool LSA = false, bool PAIR = false, int PB = 0>
 __global__ __launch_bounds__(256, 2) void k_sweep16x(SweepArgs A) {
   constexpr S16Geom g = s16_geom(KF);
   constexpr int C = SM_C, NW = SM_W, JTM = g.JTM, KP = 4 * KF, KB = KP + 2;
@@ -118,6 +120,7 @@ __global__ __launch_bounds__(256, 2) void k_sweep16x(SweepArgs A) {
   const double* brow = bimg + lr * KB + lh * KF;
   const double* xrow = xs + lr * d;
 
+  if constexpr (PB == 1 || PB == 3) { if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1); }
   if (mine > 0) issue(0);
   for (int k = 0; k < mine; ++k) {
     __builtin_amdgcn_s_waitcnt(0xF70);                 // vmcnt(0): sub-tile k landed
@@ -179,7 +182,8 @@ __global__ __launch_bounds__(256, 2) void k_sweep16x(SweepArgs A) {
     // MFMAs fill its gaps; +1.5 % in round 3's A/B)
     double de[4];
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(2);
+    if constexpr (PB == 0) __builtin_amdgcn_s_setprio(2);
+    if constexpr (PB == 1) { if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(3); else __builtin_amdgcn_s_setprio(2); }
     if (rv == SM_R) {                                  // full sub-tile: no masks
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -211,7 +215,8 @@ __global__ __launch_bounds__(256, 2) void k_sweep16x(SweepArgs A) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (PB == 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PB == 1 || PB == 3) { if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1); else __builtin_amdgcn_s_setprio(0); }
     // ---- backward
 #pragma unroll
     for (int s = 0; s < 4; ++s)
