@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Where pass F of the 64-chain full-data sweep (sweep.hip: k_gemm_fwd) spends its time:
+writes tools/_bin/gemm_ab_src/gemm_ab.hip -- the product sweep.hip included as is, plus an
+ablation copy k_gemm_fwd_x<FAM, ABL> made by text substitution from the product kernel (bit 0:
+no beta^T LDS-DMA, 1: no X LDS-DMA, 2: no tile epilogue, 3: no MFMAs; ablated arms compute
+garbage and are timed only) -- and a harness that times the product pass F, the ablations and
+pass B at configs[4]'s shape (d = 1000, 64 chains) on synthetic rows; builds it with hipcc.
+The product source is not changed.
+
+usage: tools/gemm_fwd_ab.py   (then on the GPU: tools/_bin/gemm_ab [rows_per_shard] [shards] [rounds])"""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tools", "_bin", "gemm_ab_src")
+
+
+def ablation_copy(src):
+    i = src.index("template <int FAM>\n__global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A) {")
+    j = src.index("\n}\n", i) + 3
+    k = src[i:j]
+    k = k.replace("template <int FAM>\n__global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A) {",
+                  "template <int FAM, int ABL>\n__global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd_x(SweepArgs A) {")
+    old_x = "#pragma unroll\n    for (int i = 0; i < NDMA; ++i)\n      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr,"
+    assert k.count(old_x) == 1
+    k = k.replace(old_x, "#pragma unroll\n    for (int i = 0; i < NDMA; ++i)\n      if constexpr (!(ABL & 2)) __builtin_amdgcn_raw_ptr_buffer_load_lds(xr,")
+    old_b = "#pragma unroll\n    for (int i = 0; i < NDMA; ++i)\n      __builtin_amdgcn_raw_ptr_buffer_load_lds(br,"
+    assert k.count(old_b) == 1
+    k = k.replace(old_b, "#pragma unroll\n    for (int i = 0; i < NDMA; ++i)\n      if constexpr (!(ABL & 1)) __builtin_amdgcn_raw_ptr_buffer_load_lds(br,")
+    old_e = "    if (kc == NKC - 1) {                                 // ---- tile epilogue"
+    assert k.count(old_e) == 1
+    k = k.replace(old_e, "    if (!(ABL & 4) && kc == NKC - 1) {                   // ---- tile epilogue")
+    old_m = "        acc[c2] = mfma_f64(a,"
+    assert k.count(old_m) == 1
+    k = k.replace(old_m, "        if constexpr (!(ABL & 8)) acc[c2] = mfma_f64(a,")
+    return "namespace stk {\n" + k + "\n}  // namespace stk\n"
+
+
+HARNESS = r'''
+#include <stdarg.h>
+#include <stdio.h>
+#include <vector>
+#include <algorithm>
+void stk_set_error(const char* fmt, ...) { va_list ap; va_start(ap, fmt); vfprintf(stderr, fmt, ap); va_end(ap); fputc('\n', stderr); }
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); exit(1); } } while (0)
+using namespace stk;
+int main(int argc, char** argv) {
+  const int64_t rows = argc > 1 ? atoll(argv[1]) : 2000000;
+  const int nsh = argc > 2 ? atoi(argv[2]) : 8;
+  const int rounds = argc > 3 ? atoi(argv[3]) : 3;
+  const int d = 1000, C = 64, Dp = (d + 2 + 7) / 8 * 8;
+  hipStream_t st; CK(hipStreamCreate(&st));
+  std::vector<double> beta(d);
+  for (int j = 0; j < d; ++j) beta[j] = ((j * 37) % 19 - 9) / (9.0 * sqrt((double)d));
+  double* beta_d; CK(hipMalloc(&beta_d, sizeof(double) * d));
+  CK(hipMemcpy(beta_d, beta.data(), sizeof(double) * d, hipMemcpyHostToDevice));
+  std::vector<ShardDev> sh(nsh);
+  for (int s = 0; s < nsh; ++s) {
+    double* X; int32_t* y;
+    CK(hipMalloc(&X, sizeof(double) * rows * d)); CK(hipMalloc(&y, sizeof(int32_t) * rows));
+    CK(stk_launch_gen_shard(X, nullptr, y, rows, d, s * rows, 20240, 0.0, beta_d, 1.0, STK_LOGREG, st));
+    sh[s] = ShardDev{X, nullptr, y, nullptr, rows, d, d + 1, d + 2};
+  }
+  ShardDev* sh_d; CK(hipMalloc(&sh_d, sizeof(ShardDev) * nsh));
+  CK(hipMemcpy(sh_d, sh.data(), sizeof(ShardDev) * nsh, hipMemcpyHostToDevice));
+  std::vector<double> qh((size_t)nsh * C * Dp, 0.0);
+  for (int g = 0; g < nsh * C; ++g) { qh[(size_t)g * Dp] = 0.01 * ((g % 5) - 2); for (int j = 0; j < d; ++j) qh[(size_t)g * Dp + 1 + j] = beta[j] * (0.9 + 0.002 * g); }
+  double *q, *partial; CK(hipMalloc(&q, sizeof(double) * qh.size()));
+  CK(hipMemcpy(q, qh.data(), sizeof(double) * qh.size(), hipMemcpyHostToDevice));
+  int T, LD, G; size_t lds; stk_sweep_geometry(rows, d, &T, &LD, &G, &lds, C);
+  CK(hipMalloc(&partial, sizeof(double) * (size_t)nsh * G * C * (d + 2)));
+  void* wsb; CK(hipMalloc(&wsb, stk_sweep_ws_bytes(rows, d, C, nsh)));
+  SweepWs ws = stk_sweep_ws(wsb, rows, d, nsh);
+  SweepArgs A{sh_d, q, partial, nullptr, 0, C, Dp, G, LD, d + 2, 0, G, nullptr};
+  A.qT = ws.qT; A.R = ws.R; A.Rrows = ws.Rrows;
+  hipLaunchKernelGGL(k_qt_swizzle, dim3((g5_kp(d) * G5_C + 255) / 256, nsh), dim3(256), 0, st, A, d);
+  CK(hipStreamSynchronize(st));
+  const double flops = 2.0 * rows * nsh * (double)g5_kp(d) * C;
+  struct Arm { const char* name; const void* k; int kind; std::vector<float> ms; };
+  std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG>, 0, {}},
+                           {"F-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 1>, 0, {}},
+                           {"F-noX", (const void*)k_gemm_fwd_x<STK_LOGREG, 2>, 0, {}},
+                           {"F-noXB", (const void*)k_gemm_fwd_x<STK_LOGREG, 3>, 0, {}},
+                           {"F-noEpi", (const void*)k_gemm_fwd_x<STK_LOGREG, 4>, 0, {}},
+                           {"F-noMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 8>, 0, {}},
+                           {"F-onlyMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 7>, 0, {}},
+                           {"B", (const void*)k_gemm_bwd, 1, {}}};
+  for (auto& a : arms) CK(hipFuncSetAttribute(a.k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  const int njb = (d + G5_BJB - 1) / G5_BJB;
+  auto launch = [&](const Arm& a) {
+    if (a.kind == 0) hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.k)), dim3(nsh * G), dim3(64 * G5_FW), lds, st, A);
+    else hipLaunchKernelGGL(k_gemm_bwd, dim3(nsh * G * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
+  };
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  printf("rows/shard %lld shards %d d %d C %d: G %d, %.1f GFLOP per pass\n", (long long)rows, nsh, d, C, G, flops / 1e9);
+  for (int r = 0; r < rounds; ++r)
+    for (auto& a : arms) {
+      launch(a); CK(hipStreamSynchronize(st));
+      CK(hipEventRecord(e0, st)); for (int i = 0; i < 3; ++i) launch(a); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1)); a.ms.push_back(ms / 3);
+      printf("round %d %-10s %8.3f ms %6.1f TF\n", r, a.name, ms / 3, flops / (ms / 3) / 1e9); fflush(stdout);
+    }
+  for (auto& a : arms) { auto v = a.ms; std::sort(v.begin(), v.end()); printf("median %-10s %8.3f ms %6.1f TF\n", a.name, v[v.size() / 2], flops / v[v.size() / 2] / 1e9); }
+  return 0;
+}
+'''
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    src = open(os.path.join(ROOT, "stark_amd", "csrc", "sweep.hip")).read()
+    c = os.path.join(ROOT, "stark_amd", "csrc")
+    body = ('#include "%s"\n#include "%s"\n#include "%s"\n' % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"),
+                                                          os.path.join(c, "datagen.hip"))
+            + ablation_copy(src) + HARNESS)
+    f = os.path.join(OUT, "gemm_ab.hip")
+    open(f, "w").write(body)
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", f, "-o",
+                    os.path.join(ROOT, "tools", "_bin", "gemm_ab")], check=True)
+    print("built tools/_bin/gemm_ab")
+
+
+if __name__ == "__main__":
+    main()
