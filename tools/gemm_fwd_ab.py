@@ -29,7 +29,9 @@ def ablation_copy(src):
     k = k.replace(old_b, "#pragma unroll\n    for (int i = 0; i < NDMA; ++i)\n      if constexpr (!(ABL & 1)) __builtin_amdgcn_raw_ptr_buffer_load_lds(br,")
     old_e = "    if (kc == NKC - 1) {                                 // ---- tile epilogue"
     assert k.count(old_e) == 1
-    k = k.replace(old_e, "    if (!(ABL & 4) && kc == NKC - 1) {                   // ---- tile epilogue")
+    # ABL 4: the epilogue reduced to folding the accumulators into lp (so the MFMAs stay live)
+    k = k.replace(old_e, "    if ((ABL & 4) && kc == NKC - 1) {\n#pragma unroll\n      for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] += acc[c2][0] + acc[c2][1] + acc[c2][2] + acc[c2][3];\n    }\n"
+                         "    if (!(ABL & 4) && kc == NKC - 1) {                   // ---- tile epilogue")
     old_m = "        acc[c2] = mfma_f64(a,"
     assert k.count(old_m) == 1
     k = k.replace(old_m, "        if constexpr (!(ABL & 8)) acc[c2] = mfma_f64(a,")
@@ -84,6 +86,7 @@ int main(int argc, char** argv) {
                            {"F-noEpi", (const void*)k_gemm_fwd_x<STK_LOGREG, 4>, 0, {}},
                            {"F-noMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 8>, 0, {}},
                            {"F-onlyMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 7>, 0, {}},
+                           {"F-noEpi-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 5>, 0, {}},
                            {"B", (const void*)k_gemm_bwd, 1, {}}};
   for (auto& a : arms) CK(hipFuncSetAttribute(a.k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   const int njb = (d + G5_BJB - 1) / G5_BJB;
