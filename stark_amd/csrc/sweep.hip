@@ -648,66 +648,6 @@ __global__ __launch_bounds__(512) void k_sweep3(SweepArgs A, int NBrt) {
   }
 }
 
-// Logistic residual v3 (the 64-chain pass F epilogue; round 3's 16-chain sweep): round 2's v2 with fewer VALU instructions -- on gfx950 EVERY
-// vector instruction (f64, f32, int, select) takes the issue slot the f64 MFMA needs
-// (tools/valu_mix.hip: no class overlaps v_mfma_f64_16x16x4), so the residual's instruction
-// count, not its f64 count, is what it costs.  Same quantities and cutoffs as v2:
-//   Stan's lower cutoff without selects: a = min(|t| + 2^60 max(-20 - t, 0), 700) is |t| for
-//   t >= -20 and 700 below, where e = exp(-700) ~ 1e-304 makes lg = e, lt = t - lg = t and
-//   dv/sgn = 1/(1 + e) = 1 exactly -- Stan's (t, 1);
-//   exp(-a): 256-entry 2^{j/256} table, |r| <= ln2/512, degree-4 Taylor (rel. error 4e-17), the
-//   2^{n div 256} scale by v_ldexp_f64;  log1p(e): 257-entry [c_j, d_j, l_j] table (j = rint(256 e)),
-//   |rl| <= 1/512, degree-4 fitted q (abs. error 1.2e-18);
-//   lt = t/2 - (|t|/2 + lg) = min(t, 0) - lg with NaN kept (a NaN eta gives a NaN lp; t = +inf
-//   gives NaN where Stan's upper branch gives 0 -- a point no finite beta reaches).
-// About 38 vector instructions per (row, chain) against v2's ~50.
-constexpr int LG3_TAB = 256 + 4 * 257;     // doubles: T[256], then [c_j, d_j, l_j, 0] for j = 0..256
-__device__ void logit3_tables_init(double* tab) {
-  for (int i = threadIdx.x; i < LG3_TAB; i += blockDim.x) {
-    double v;
-    if (i < 256) {
-      v = exp2((double)i / 256.0);
-    } else {
-      const int j = (i - 256) >> 2, f = (i - 256) & 3;
-      v = f == 0 ? 256.0 / (256 + j) : (f == 1 ? (double)j / (256 + j) : (f == 2 ? log1p((double)j / 256.0) : 0.0));
-    }
-    tab[i] = v;
-  }
-}
-
-// v_rcp_f64 alone is good to ~2^-24 only (tools/rcp_acc.hip, profiles/r03s_rcp_acc.log: 2.6e8 ulp;
-// 11 ulp after the one Newton step below).
-__device__ __forceinline__ void logit_resid3(double eta, uint32_t ymask, const double* tab, double& lt, double& dv) {
-  constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
-  constexpr double INV_L = 369.3299304675746;             // 256 / ln 2
-  constexpr double L_HI = 0.0027076061742263846;          // ln2/256 to 32 significant bits: n L_HI exact
-  constexpr double L_LO = -1.6409824498184568e-13;        // ln2/256 - L_HI
-  constexpr double Q1 = -0.4999999999996968, Q2 = 0.33333333333269194, Q3 = -0.25000063579045223,
-                   Q4 = 0.2000006787837857;               // log(1+x)/x on |x| <= 1/512 (tools: least squares)
-  const double t = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, eta) ^ ((uint64_t)ymask << 32));
-  const double a = fmin(fma(fmax(-20.0 - t, 0.0), 1152921504606846976.0, fabs(t)), 700.0);   // + 2^60 max(-20 - t, 0)
-  const double sn = fma(-a, INV_L, MAGIC);
-  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
-  const double n = sn - MAGIC;
-  double r = fma(-n, L_HI, -a);
-  r = fma(-n, L_LO, r);
-  const double p = fma(fma(fma(fma(1.0 / 24.0, r, 1.0 / 6.0), r, 0.5), r, 1.0), r, 1.0);
-  const double e = __builtin_amdgcn_ldexp(tab[ni & 255] * p, ni >> 8);
-  const int j = (int)fma(e, 256.0, 0.5);                  // rint(256 e), e in [0, 1] (v_cvt_i32_f64 truncates)
-  const double* cj = tab + 256 + 4 * j;
-  const dbl2 cd = *reinterpret_cast<const dbl2*>(cj);
-  const double rl = fma(e, cd.x, -cd.y);
-  const double q = fma(fma(fma(fma(Q4, rl, Q3), rl, Q2), rl, Q1), rl, 1.0);
-  const double lg = fma(rl, q, cj[2]);
-  const double u = 1.0 + e;
-  double ri = __builtin_amdgcn_rcp(u);
-  ri = fma(ri, fma(-u, ri, 1.0), ri);
-  const double w = e * ri;
-  const uint32_t neg = (uint32_t)((int32_t)(__builtin_bit_cast(uint64_t, t) >> 32) >> 31);   // ~0u when t < 0
-  const double dvp = blend(neg, ri, w);
-  dv = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, dvp) ^ ((uint64_t)ymask << 32));
-  lt = fma(0.5, t, fma(-0.5, fabs(t), -lg));
-}
 
 // v5 sweep: 64 chains of a shard, any d -- two fp64 MFMA GEMM passes (BASELINE configs[4]:
 // full-data logistic regression, d = 1000, 64 chains).
@@ -783,8 +723,7 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
   constexpr int KCF = G5_FKC, STG = g5_fstage_bytes(), XB = STG / 2;   // stage: [X 64 x KCF][beta^T KCF x 64]
   constexpr int PPR = KCF / 2;                          // 16-B pieces per X row in the stage
   constexpr int NDMA = (XB / 1024) / NW;                // DMA instructions per wave per operand image
-  constexpr int EV = STG / NW / 512;                    // eta values per wave per epilogue round
-  static_assert(NDMA >= 1 && EV >= 1 && (4 * NCT) % EV == 0, "pass F stage geometry");
+  static_assert(NDMA >= 1, "pass F stage geometry");
   // X piece swizzle: 256-B rows (PPR 16) XOR the piece with row & 15; 128-B rows (PPR 8) put
   // rows of one parity on one half of the banks, so XOR with (row >> 1) & 7
   auto swz = [](int row) { return PPR == 16 ? (row & 15) : ((row >> 1) & 7); };
@@ -806,7 +745,7 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
   extern __shared__ __attribute__((aligned(16))) double lds[];
   char* const stg = reinterpret_cast<char*>(lds);                 // NS stages of STG bytes
   double* const sptab = reinterpret_cast<double*>(stg + NS * STG);
-  if constexpr (FAM == STK_LOGREG) logit3_tables_init(sptab);
+  if constexpr (FAM == STK_LOGREG) exp_table_init(sptab);
 
   // per-lane chain constants: chain 16 ct + lr, ct = 2 wc + c2
   const double* qb = A.q + (size_t)shard * G5_C * A.Dp;
@@ -842,14 +781,17 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
                                                kc * KCF * 512 + (w * NDMA + i) * 1024, 0, 0);
   };
 
-  double lpa[NCT], gaa[NCT];
+  // per chain tile: logistic lm = sum(t - |t|), sp = prod(1 + e) - 1, ll = the flushed log1p(sp)
+  // (residual v4, sweep_common.h); linear: lm = sum z^2
+  double lm[NCT], sp[NCT], ll[NCT], gaa[NCT];
 #pragma unroll
-  for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] = gaa[c2] = 0.0;
+  for (int c2 = 0; c2 < NCT; ++c2) lm[c2] = sp[c2] = ll[c2] = gaa[c2] = 0.0;
   char* const Rimg = reinterpret_cast<char*>(A.R + ((size_t)shard * A.Rrows + r0) * G5_C);
   const int nst = ntile * NKC;
   for (int s0 = 0; s0 < NS - 1 && s0 < nst; ++s0) issue(s0);
   dbl4 acc[NCT];
   double yt[4] = {0.0, 0.0, 0.0, 0.0};                  // y of this lane's 4 rows of the current tile
+  uint32_t yit[4] = {0u, 0u, 0u, 0u};
   for (int st = 0; st < nst; ++st) {
     const int kc = st % NKC;
     if (kc == 0) {
@@ -864,7 +806,8 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t grow = tb + 4 * i;
-        yt[i] = grow < nrows ? ((FAM == STK_LOGREG) ? (double)sh.yi[r0 + grow] : sh.y[r0 + grow]) : 0.0;
+        if constexpr (FAM == STK_LOGREG) yit[i] = grow < nrows ? (uint32_t)sh.yi[r0 + grow] : 0u;
+        else yt[i] = grow < nrows ? sh.y[r0 + grow] : 0.0;
       }
     }
     const char* b = stg + (st % NS) * STG;
@@ -878,53 +821,50 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
         acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + XB + g5_chain_off(kk, 16 * (NCT * wc + c2) + lr)), acc[c2]);
     }
     if (kc == NKC - 1) {                                 // ---- tile epilogue: residual, R, lp
-      lds_barrier();                                     // every wave is done reading stage st
-      // eta goes through this wave's own STG / NW bytes of the stage just consumed (refilled
-      // only after the next barrier), EV values per round, so the residuals run one at a time
-      // from LDS instead of holding 4 NCT softplus evaluations' temporaries in registers
+      // straight from the accumulators, every (chain tile, row) unrolled: compile-time indices
+      // into alpha / lm / sp, and residual v4 (one exp per element, the logs as a running
+      // product per chain tile, flushed every 64 tiles = 256 elements)
       const int tile = st / NKC;
-      char* const b2 = stg + (st % NS) * STG;
-      auto eslot = [&](int e) -> double* { return reinterpret_cast<double*>(b2 + w * (EV * 512) + (e % EV) * 512) + lane; };
 #pragma unroll
-      for (int e0 = 0; e0 < 4 * NCT; e0 += EV) {
+      for (int c2 = 0; c2 < NCT; ++c2) {
+        const int ct = NCT * wc + c2;
 #pragma unroll
-        for (int e = e0; e < e0 + EV; ++e) *eslot(e) = acc[e >> 2][e & 3];
-#pragma unroll 1
-        for (int e = e0; e < e0 + EV; ++e) {
-          const int c2 = e >> 2, i = e & 3, ct = NCT * wc + c2;
+        for (int i = 0; i < 4; ++i) {
           const int row = 16 * wr + lh + 4 * i;              // row of the tile
           const int64_t grow = (int64_t)tile * G5_TR + row;  // row of the chunk
           const bool valid = grow < nrows;
-          const double yv = i == 0 ? yt[0] : (i == 1 ? yt[1] : (i == 2 ? yt[2] : yt[3]));
-          double al = alpha[0], isg = inv_s[0];
-#pragma unroll
-          for (int q = 1; q < NCT; ++q)
-            if (c2 == q) {
-              al = alpha[q];
-              isg = inv_s[q];
-            }
-          const double eta = *eslot(e) + al;
-          double dv, lt;
+          const double eta = acc[c2][i] + alpha[c2];
+          double dv;
           if constexpr (FAM == STK_LOGREG) {
-            logit_resid3(eta, yv == 0.0 ? 0x80000000u : 0u, sptab, lt, dv);
+            double lm2 = lm[c2], sp2 = sp[c2];
+            dv = -logit_resid4(eta, yit[i], sptab, lm2, sp2);
+            lm[c2] = valid ? lm2 : lm[c2];
+            sp[c2] = valid ? sp2 : sp[c2];
           } else {
-            const double z = (yv - eta) * isg;
-            lt = z * z;
-            dv = z * isg;
+            const double z = (yt[i] - eta) * inv_s[c2];
+            lm[c2] += valid ? z * z : 0.0;
+            dv = z * inv_s[c2];
           }
           dv = valid ? dv : 0.0;
-          lt = valid ? lt : 0.0;
-#pragma unroll
-          for (int q = 0; q < NCT; ++q) {
-            lpa[q] += q == c2 ? lt : 0.0;
-            gaa[q] += q == c2 ? dv : 0.0;
-          }
+          gaa[c2] += dv;
           *reinterpret_cast<double*>(Rimg + g5_chain_off((int)grow, 16 * ct + lr)) = dv;
+        }
+      }
+      if constexpr (FAM == STK_LOGREG) {
+        if ((tile & 63) == 63) {
+#pragma unroll
+          for (int c2 = 0; c2 < NCT; ++c2) {
+            ll[c2] += log1p(sp[c2]);
+            sp[c2] = 0.0;
+          }
         }
       }
       __builtin_amdgcn_s_waitcnt(0xF70);                  // vmcnt(0): R stores retired before the next counted DMA wait
     }
   }
+  double lpa[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] = (FAM == STK_LOGREG) ? 0.5 * lm[c2] - (ll[c2] + log1p(sp[c2])) : lm[c2];
 
   // ---- lp and sum(d eta) per chain: lanes lr of the 4 row groups h of the 4 waves wr, fixed order
   __syncthreads();
@@ -1152,7 +1092,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *T = G5_TR;
     *LD = 0;
     *G = (int)g;
-    *lds_bytes = G5_FS * g5_fstage_bytes() + LG3_TAB * sizeof(double);
+    *lds_bytes = G5_FS * g5_fstage_bytes() + EX_TAB * sizeof(double);
     return;
   }
   if (var == 4) {                       // k_sweep16 (sweep16.hip)

@@ -64,6 +64,70 @@ __device__ __forceinline__ double blend(uint32_t m, double a, double b) {   // m
   return __builtin_bit_cast(double, (ua & mm) | (ub & ~mm));
 }
 
+// exp table: T_j = 2^(j/1024), j < 1024 (8 KB of LDS per workgroup)
+constexpr int EX_TAB = 1024;
+__device__ void exp_table_init(double* tab) {
+  for (int i = threadIdx.x; i < EX_TAB; i += blockDim.x) tab[i] = exp2((double)i / (double)EX_TAB);
+}
+
+// Logistic residual v4: Stan 2.19's bernoulli_logit term and its derivative for one (row,
+// chain), t = (2y - 1) eta:
+//   t > 20:   lt = -exp(-t),             dv/sgn = exp(-t)
+//   t < -20:  lt = t,                    dv/sgn = 1
+//   else:     lt = -log1p(exp(-t)),      dv/sgn = exp(-t) / (exp(-t) + 1)
+// computed branch-free from e = exp(-|t|) as lt = min(t, 0) - log1p(e), dv/sgn = (t < 0 ?
+// 1/(1+e) : e/(1+e)); above 20 the smooth form differs from Stan's by <= e^2/2 < 2.2e-18.
+// The kernel works with s = -t = (1 - 2y) eta, whose sign bit is eta's plus y << 31 (one
+// v_lshl_add_u32: adding 2^31 to the high word flips the sign), and returns -dv the same way;
+// the kernel negates the gradient sums once at the end.
+//
+// The log is not taken per element.  Per lane (one chain) the kernel keeps
+//   lm = sum (t - |t|)              = 2 sum min(t, 0), exact per term, a NaN eta stays NaN
+//   sp = prod (1 + e) - 1           one fma per element: sp <- sp (1 + e) + e
+// and adds log1p(sp) to the lane's lp every 64 sub-tiles (256 elements: 1 + sp < 2^256, and
+// every step adds at most eps of relative error to 1 + sp, so log1p(sp) is off by <= 256 eps
+// absolute); lp = lm/2 - sum log1p(sp).  Rows with e below eps are summed exactly (1 + e = 1,
+// sp += e).  Against residual v3 this drops the table log1p (its index, two LDS reads, a degree-4
+// polynomial) and the per-element lp terms: ~27 instead of ~43 vector instructions per element.
+//   exp(-a), a = min(|t|, 700): n = rint(-a 1024/ln2) by the 1.5 2^52 trick, r = -a - n ln2/1024
+//   (|r| <= ln2/2048; ln2/1024 rounded once: |error of r| <= n ulp(ln2/1024)/2, 1.6e-15 relative at
+//   a = 20), e^r by a fitted degree-3 polynomial (relative error 9.4e-17), times T_{n mod 1024}, times
+//   2^{n div 1024} by v_ldexp_f64 -- whose exponent is -1100 for t < -20, making e = 0: then
+//   lt = min(t, 0) = t and dv/sgn = 1/(1 + 0) = 1 exactly, Stan's lower branch;
+//   1/(1 + e): v_rcp_f64 + one Newton step (11 ulp, tools/rcp_acc.hip).
+__device__ __forceinline__ double fmin_abs(double x, double c) {   // min(|x|, c), NaN x -> c
+  // one v_min_f64 with the abs modifier (fmin() adds a canonicalising v_max_f64 in IEEE mode)
+  double r;
+  asm("v_min_f64 %0, |%1|, %2" : "=v"(r) : "v"(x), "s"(c));
+  return r;
+}
+__device__ __forceinline__ double logit_resid4(double eta, uint32_t y, const double* tab, double& lm, double& sp) {
+  constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
+  constexpr double INV_L = 1477.3197218702985;            // 1024 / ln 2
+  constexpr double L = 0.0006769015435155716;             // ln 2 / 1024
+  constexpr double C2 = 0.5000000039583942, C3 = 0.16666666713444417;   // e^r on |r| <= ln2/2048 (fit)
+  const uint64_t eb = __builtin_bit_cast(uint64_t, eta);
+  const double s = __builtin_bit_cast(double, (eb & 0xFFFFFFFFull) | ((uint64_t)((y << 31) + (uint32_t)(eb >> 32)) << 32));
+  const double a = fmin_abs(s, 700.0);                    // |s| = |eta|; NaN -> 700 (the NaN stays in lm)
+  const double sn = fma(-a, INV_L, MAGIC);
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
+  const double n = sn - MAGIC;
+  const double r = fma(-n, L, -a);
+  const double p = fma(fma(fma(C3, r, C2), r, 1.0), r, 1.0);
+  const int ke = (s > 20.0) ? -1100 : (ni >> 10);         // Stan's lower cutoff (t < -20): e = 0
+  const double e = __builtin_amdgcn_ldexp(tab[ni & (EX_TAB - 1)] * p, ke);
+  const double u = 1.0 + e;
+  double ri = __builtin_amdgcn_rcp(u);
+  ri = fma(ri, fma(-u, ri, 1.0), ri);
+  const double w = e * ri;
+  const uint64_t sb = __builtin_bit_cast(uint64_t, s);
+  const uint32_t spos = (uint32_t)((int32_t)(sb >> 32) >> 31);   // ~0u when s < 0, i.e. t > 0
+  const uint64_t dvp = __builtin_bit_cast(uint64_t, blend(spos, w, ri));   // dv/sgn
+  lm += -s - fabs(s);                                     // t - |t|
+  sp = fma(sp, u, e);
+  return __builtin_bit_cast(double, (dvp & 0xFFFFFFFFull) | ((uint64_t)((y << 31) + (uint32_t)(dvp >> 32)) << 32));   // -dv
+}
+
 }  // namespace stk
 
 // The 16-chain sweep (sweep16.hip): shapes it covers, its LDS bytes, its launch.

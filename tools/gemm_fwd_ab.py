@@ -30,7 +30,7 @@ def ablation_copy(src):
     old_e = "    if (kc == NKC - 1) {                                 // ---- tile epilogue"
     assert k.count(old_e) == 1
     # ABL 4: the epilogue reduced to folding the accumulators into lp (so the MFMAs stay live)
-    k = k.replace(old_e, "    if ((ABL & 4) && kc == NKC - 1) {\n#pragma unroll\n      for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] += acc[c2][0] + acc[c2][1] + acc[c2][2] + acc[c2][3];\n    }\n"
+    k = k.replace(old_e, "    if ((ABL & 4) && kc == NKC - 1) {\n#pragma unroll\n      for (int c2 = 0; c2 < NCT; ++c2) gaa[c2] += acc[c2][0] + acc[c2][1] + acc[c2][2] + acc[c2][3];\n    }\n"
                          "    if (!(ABL & 4) && kc == NKC - 1) {                   // ---- tile epilogue")
     old_m = "        acc[c2] = mfma_f64(a,"
     assert k.count(old_m) == 1
@@ -79,6 +79,7 @@ int main(int argc, char** argv) {
   CK(hipStreamSynchronize(st));
   const double flops = 2.0 * rows * nsh * (double)g5_kp(d) * C;
   struct Arm { const char* name; const void* k; int kind; std::vector<float> ms; };
+#define HAVE_OLD @OLD@
   std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG>, 0, {}},
                            {"F-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 1>, 0, {}},
                            {"F-noX", (const void*)k_gemm_fwd_x<STK_LOGREG, 2>, 0, {}},
@@ -88,6 +89,9 @@ int main(int argc, char** argv) {
                            {"F-onlyMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 7>, 0, {}},
                            {"F-noEpi-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 5>, 0, {}},
                            {"B", (const void*)k_gemm_bwd, 1, {}}};
+#if HAVE_OLD
+  arms.insert(arms.begin() + 1, Arm{"F-old", (const void*)k_gemm_fwd_old<STK_LOGREG>, 0, {}});
+#endif
   for (auto& a : arms) CK(hipFuncSetAttribute(a.k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   const int njb = (d + G5_BJB - 1) / G5_BJB;
   auto launch = [&](const Arm& a) {
@@ -95,6 +99,26 @@ int main(int argc, char** argv) {
     else hipLaunchKernelGGL(k_gemm_bwd, dim3(nsh * G * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
   };
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  {   // parity of the arms that compute: F (and F-old) + pass B + the chunk reduction
+    double *lp, *grad; CK(hipMalloc(&lp, sizeof(double) * nsh * C)); CK(hipMalloc(&grad, sizeof(double) * nsh * C * Dp));
+    std::vector<std::vector<double>> res;
+    for (int k = 0; k < (HAVE_OLD ? 2 : 1); ++k) {
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(arms[k].k)), dim3(nsh * G), dim3(64 * G5_FW), lds, st, A);
+      hipLaunchKernelGGL(k_gemm_bwd, dim3(nsh * G * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
+      CK(stk_launch_sweep_reduce(STK_LOGREG, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
+      std::vector<double> h((size_t)nsh * C * (Dp + 1));
+      CK(hipMemcpy(h.data(), lp, sizeof(double) * nsh * C, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h.data() + nsh * C, grad, sizeof(double) * nsh * C * Dp, hipMemcpyDeviceToHost));
+      res.push_back(h);
+    }
+    if (res.size() == 2) {
+      double lpr = 0, gr = 0, gmax = 0;
+      for (int i = 0; i < nsh * C; ++i) lpr = std::max(lpr, fabs(res[1][i] - res[0][i]) / fabs(res[1][i]));
+      for (size_t i = nsh * C; i < res[0].size(); ++i) gmax = std::max(gmax, fabs(res[1][i]));
+      for (size_t i = nsh * C; i < res[0].size(); ++i) gr = std::max(gr, fabs(res[1][i] - res[0][i]) / gmax);
+      printf("parity F vs F-old: lp max rel %.3g, grad max |diff| / max|grad| %.3g (lp[0] %.6f)\n", lpr, gr, res[0][0]);
+    }
+  }
   printf("rows/shard %lld shards %d d %d C %d: G %d, %.1f GFLOP per pass\n", (long long)rows, nsh, d, C, G, flops / 1e9);
   for (int r = 0; r < rounds; ++r)
     for (auto& a : arms) {
@@ -109,13 +133,25 @@ int main(int argc, char** argv) {
 '''
 
 
+def old_copy(ref="HEAD"):
+    """The committed (git `ref`) pass F as k_gemm_fwd_old<FAM>, for a before/after arm."""
+    src = subprocess.run(["git", "-C", ROOT, "show", ref + ":stark_amd/csrc/sweep.hip"], check=True,
+                         capture_output=True, text=True).stdout
+    i = src.index("template <int FAM>\n__global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A) {")
+    j = src.index("\n}\n", i) + 3
+    k = src[i:j].replace("void k_gemm_fwd(SweepArgs A) {", "void k_gemm_fwd_old(SweepArgs A) {")
+    return "namespace stk {\n" + k + "\n}  // namespace stk\n"
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     src = open(os.path.join(ROOT, "stark_amd", "csrc", "sweep.hip")).read()
     c = os.path.join(ROOT, "stark_amd", "csrc")
     body = ('#include "%s"\n#include "%s"\n#include "%s"\n' % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"),
                                                           os.path.join(c, "datagen.hip"))
-            + ablation_copy(src) + HARNESS)
+            + '#include "%s"\n' % os.path.join(ROOT, "tools", "sweep_legacy.hip")
+            + ablation_copy(src) + (old_copy(os.environ.get("GEMM_AB_OLD", "HEAD")) if os.environ.get("GEMM_AB_OLD") else "")
+            + HARNESS.replace("@OLD@", "1" if os.environ.get("GEMM_AB_OLD") else "0"))
     f = os.path.join(OUT, "gemm_ab.hip")
     open(f, "w").write(body)
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", f, "-o",

@@ -7,6 +7,68 @@
 #pragma once
 namespace stk {
 
+// Logistic residual v3 (round 3's 16-chain sweep and pass F epilogue): round 2's v2 with fewer VALU instructions -- on gfx950 EVERY
+// vector instruction (f64, f32, int, select) takes the issue slot the f64 MFMA needs
+// (tools/valu_mix.hip: no class overlaps v_mfma_f64_16x16x4), so the residual's instruction
+// count, not its f64 count, is what it costs.  Same quantities and cutoffs as v2:
+//   Stan's lower cutoff without selects: a = min(|t| + 2^60 max(-20 - t, 0), 700) is |t| for
+//   t >= -20 and 700 below, where e = exp(-700) ~ 1e-304 makes lg = e, lt = t - lg = t and
+//   dv/sgn = 1/(1 + e) = 1 exactly -- Stan's (t, 1);
+//   exp(-a): 256-entry 2^{j/256} table, |r| <= ln2/512, degree-4 Taylor (rel. error 4e-17), the
+//   2^{n div 256} scale by v_ldexp_f64;  log1p(e): 257-entry [c_j, d_j, l_j] table (j = rint(256 e)),
+//   |rl| <= 1/512, degree-4 fitted q (abs. error 1.2e-18);
+//   lt = t/2 - (|t|/2 + lg) = min(t, 0) - lg with NaN kept (a NaN eta gives a NaN lp; t = +inf
+//   gives NaN where Stan's upper branch gives 0 -- a point no finite beta reaches).
+// About 38 vector instructions per (row, chain) against v2's ~50.
+constexpr int LG3_TAB = 256 + 4 * 257;     // doubles: T[256], then [c_j, d_j, l_j, 0] for j = 0..256
+__device__ void logit3_tables_init(double* tab) {
+  for (int i = threadIdx.x; i < LG3_TAB; i += blockDim.x) {
+    double v;
+    if (i < 256) {
+      v = exp2((double)i / 256.0);
+    } else {
+      const int j = (i - 256) >> 2, f = (i - 256) & 3;
+      v = f == 0 ? 256.0 / (256 + j) : (f == 1 ? (double)j / (256 + j) : (f == 2 ? log1p((double)j / 256.0) : 0.0));
+    }
+    tab[i] = v;
+  }
+}
+
+// v_rcp_f64 alone is good to ~2^-24 only (tools/rcp_acc.hip, profiles/r03s_rcp_acc.log: 2.6e8 ulp;
+// 11 ulp after the one Newton step below).
+__device__ __forceinline__ void logit_resid3(double eta, uint32_t ymask, const double* tab, double& lt, double& dv) {
+  constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
+  constexpr double INV_L = 369.3299304675746;             // 256 / ln 2
+  constexpr double L_HI = 0.0027076061742263846;          // ln2/256 to 32 significant bits: n L_HI exact
+  constexpr double L_LO = -1.6409824498184568e-13;        // ln2/256 - L_HI
+  constexpr double Q1 = -0.4999999999996968, Q2 = 0.33333333333269194, Q3 = -0.25000063579045223,
+                   Q4 = 0.2000006787837857;               // log(1+x)/x on |x| <= 1/512 (tools: least squares)
+  const double t = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, eta) ^ ((uint64_t)ymask << 32));
+  const double a = fmin(fma(fmax(-20.0 - t, 0.0), 1152921504606846976.0, fabs(t)), 700.0);   // + 2^60 max(-20 - t, 0)
+  const double sn = fma(-a, INV_L, MAGIC);
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
+  const double n = sn - MAGIC;
+  double r = fma(-n, L_HI, -a);
+  r = fma(-n, L_LO, r);
+  const double p = fma(fma(fma(fma(1.0 / 24.0, r, 1.0 / 6.0), r, 0.5), r, 1.0), r, 1.0);
+  const double e = __builtin_amdgcn_ldexp(tab[ni & 255] * p, ni >> 8);
+  const int j = (int)fma(e, 256.0, 0.5);                  // rint(256 e), e in [0, 1] (v_cvt_i32_f64 truncates)
+  const double* cj = tab + 256 + 4 * j;
+  const dbl2 cd = *reinterpret_cast<const dbl2*>(cj);
+  const double rl = fma(e, cd.x, -cd.y);
+  const double q = fma(fma(fma(fma(Q4, rl, Q3), rl, Q2), rl, Q1), rl, 1.0);
+  const double lg = fma(rl, q, cj[2]);
+  const double u = 1.0 + e;
+  double ri = __builtin_amdgcn_rcp(u);
+  ri = fma(ri, fma(-u, ri, 1.0), ri);
+  const double w = e * ri;
+  const uint32_t neg = (uint32_t)((int32_t)(__builtin_bit_cast(uint64_t, t) >> 32) >> 31);   // ~0u when t < 0
+  const double dvp = blend(neg, ri, w);
+  dv = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, dvp) ^ ((uint64_t)ymask << 32));
+  lt = fma(0.5, t, fma(-0.5, fabs(t), -lg));
+}
+
+
 // NEWTON: one Newton step on v_rcp_f64, which alone is good to ~2^-24 only (tools/rcp_acc.hip,
 // profiles/r03s_rcp_acc.log: 2.6e8 ulp; 11 ulp after the step); without it the gradient moves by
 // 4e-9 relative (RV 4, measurement only).  EXP4: degree-4 Taylor exp (else a fitted degree 3,
