@@ -78,32 +78,42 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(k_qt_swizzle, dim3((g5_kp(d) * G5_C + 255) / 256, nsh), dim3(256), 0, st, A, d);
   CK(hipStreamSynchronize(st));
   const double flops = 2.0 * rows * nsh * (double)g5_kp(d) * C;
-  struct Arm { const char* name; const void* k; int kind; std::vector<float> ms; };
+  // kind 0: pass F (par: computes, so checked against F), 1: pass B
+  struct Arm { const char* name; const void* k; int kind; size_t lds; bool par; std::vector<float> ms; };
 #define HAVE_OLD @OLD@
-  std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG>, 0, {}},
-                           {"F-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 1>, 0, {}},
-                           {"F-noX", (const void*)k_gemm_fwd_x<STK_LOGREG, 2>, 0, {}},
-                           {"F-noXB", (const void*)k_gemm_fwd_x<STK_LOGREG, 3>, 0, {}},
-                           {"F-noEpi", (const void*)k_gemm_fwd_x<STK_LOGREG, 4>, 0, {}},
-                           {"F-noMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 8>, 0, {}},
-                           {"F-onlyMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 7>, 0, {}},
-                           {"F-noEpi-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 5>, 0, {}},
-                           {"B", (const void*)k_gemm_bwd, 1, {}}};
+  // the committed pass F's LDS: its stages + its own table (round 3's residual v3 tables are
+  // 1284 doubles, v4's 1024: launched with v4's size, v3's log entries fell outside the block)
+  const size_t lds_old = std::max(lds, (size_t)G5_FS * g5_fstage_bytes() + @OLDTAB@ * sizeof(double));
+  std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG>, 0, lds, true, {}}};
 #if HAVE_OLD
-  arms.insert(arms.begin() + 1, Arm{"F-old", (const void*)k_gemm_fwd_old<STK_LOGREG>, 0, {}});
+  arms.push_back(Arm{"F-old", (const void*)k_gemm_fwd_old<STK_LOGREG>, 0, lds_old, true, {}});
 #endif
+  arms.push_back(Arm{"F-r1k32s2", gemm_fwd_t_ptr<2, 32, 1>(), 0, gemm_fwd_t_lds<2, 32, 1>(), true, {}});
+  arms.push_back(Arm{"F-r2k16s2", gemm_fwd_t_ptr<2, 16, 2>(), 0, gemm_fwd_t_lds<2, 16, 2>(), true, {}});
+  arms.push_back(Arm{"F-r2k16s3", gemm_fwd_t_ptr<3, 16, 2>(), 0, gemm_fwd_t_lds<3, 16, 2>(), true, {}});
+  if (getenv("GEMM_AB_ABL")) {
+    arms.push_back(Arm{"F-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 1>, 0, lds, false, {}});
+    arms.push_back(Arm{"F-noEpi", (const void*)k_gemm_fwd_x<STK_LOGREG, 4>, 0, lds, false, {}});
+    arms.push_back(Arm{"F-onlyMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 7>, 0, lds, false, {}});
+  }
+  arms.push_back(Arm{"B", (const void*)k_gemm_bwd, 1, 0, false, {}});
   for (auto& a : arms) CK(hipFuncSetAttribute(a.k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   const int njb = (d + G5_BJB - 1) / G5_BJB;
   auto launch = [&](const Arm& a) {
-    if (a.kind == 0) hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.k)), dim3(nsh * G), dim3(64 * G5_FW), lds, st, A);
+    if (a.kind == 0) hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.k)), dim3(nsh * G), dim3(64 * G5_FW), a.lds, st, A);
     else hipLaunchKernelGGL(k_gemm_bwd, dim3(nsh * G * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
   };
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   {   // parity of the arms that compute: F (and F-old) + pass B + the chunk reduction
     double *lp, *grad; CK(hipMalloc(&lp, sizeof(double) * nsh * C)); CK(hipMalloc(&grad, sizeof(double) * nsh * C * Dp));
     std::vector<std::vector<double>> res;
-    for (int k = 0; k < (HAVE_OLD ? 2 : 1); ++k) {
-      hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(arms[k].k)), dim3(nsh * G), dim3(64 * G5_FW), lds, st, A);
+    std::vector<const char*> names;
+    for (const Arm& a : arms) {
+      if (!a.par) continue;
+      names.push_back(a.name);
+      CK(hipMemset(ws.R, 0xFF, sizeof(double) * (size_t)nsh * ws.Rrows * C));   // NaN: an unwritten R row shows
+      launch(a);
+      CK(hipGetLastError());
       hipLaunchKernelGGL(k_gemm_bwd, dim3(nsh * G * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
       CK(stk_launch_sweep_reduce(STK_LOGREG, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
       std::vector<double> h((size_t)nsh * C * (Dp + 1));
@@ -111,12 +121,12 @@ int main(int argc, char** argv) {
       CK(hipMemcpy(h.data() + nsh * C, grad, sizeof(double) * nsh * C * Dp, hipMemcpyDeviceToHost));
       res.push_back(h);
     }
-    if (res.size() == 2) {
+    for (size_t k = 1; k < res.size(); ++k) {
       double lpr = 0, gr = 0, gmax = 0;
-      for (int i = 0; i < nsh * C; ++i) lpr = std::max(lpr, fabs(res[1][i] - res[0][i]) / fabs(res[1][i]));
-      for (size_t i = nsh * C; i < res[0].size(); ++i) gmax = std::max(gmax, fabs(res[1][i]));
-      for (size_t i = nsh * C; i < res[0].size(); ++i) gr = std::max(gr, fabs(res[1][i] - res[0][i]) / gmax);
-      printf("parity F vs F-old: lp max rel %.3g, grad max |diff| / max|grad| %.3g (lp[0] %.6f)\n", lpr, gr, res[0][0]);
+      for (int i = 0; i < nsh * C; ++i) lpr = std::max(lpr, fabs(res[k][i] - res[0][i]) / fabs(res[0][i]));
+      for (size_t i = nsh * C; i < res[0].size(); ++i) gmax = std::max(gmax, fabs(res[0][i]));
+      for (size_t i = nsh * C; i < res[0].size(); ++i) gr = std::max(gr, fabs(res[k][i] - res[0][i]) / gmax);
+      printf("parity %s vs F: lp max rel %.3g, grad max |diff| / max|grad| %.3g (lp[0] %.6f)\n", names[k], lpr, gr, res[0][0]);
     }
   }
   printf("rows/shard %lld shards %d d %d C %d: G %d, %.1f GFLOP per pass\n", (long long)rows, nsh, d, C, G, flops / 1e9);
@@ -143,15 +153,26 @@ def old_copy(ref="HEAD"):
     return "namespace stk {\n" + k + "\n}  // namespace stk\n"
 
 
+def old_table():
+    """Doubles of the committed pass F's LDS table (the lds_bytes line of stk_sweep_geometry's C = 64 branch)."""
+    ref = os.environ.get("GEMM_AB_OLD")
+    if not ref:
+        return "0"
+    src = subprocess.run(["git", "-C", ROOT, "show", ref + ":stark_amd/csrc/sweep.hip"], check=True,
+                         capture_output=True, text=True).stdout
+    line = [l for l in src.splitlines() if "*lds_bytes = G5_FS * g5_fstage_bytes() +" in l][0]
+    return "(" + line.split("+", 1)[1].split("*")[0].strip() + ")"
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     src = open(os.path.join(ROOT, "stark_amd", "csrc", "sweep.hip")).read()
     c = os.path.join(ROOT, "stark_amd", "csrc")
     body = ('#include "%s"\n#include "%s"\n#include "%s"\n' % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"),
                                                           os.path.join(c, "datagen.hip"))
-            + '#include "%s"\n' % os.path.join(ROOT, "tools", "sweep_legacy.hip")
+            + '#include "%s"\n#include "%s"\n' % (os.path.join(ROOT, "tools", "sweep_legacy.hip"), os.path.join(ROOT, "tools", "gemm_fwd_variants.hip"))
             + ablation_copy(src) + (old_copy(os.environ.get("GEMM_AB_OLD", "HEAD")) if os.environ.get("GEMM_AB_OLD") else "")
-            + HARNESS.replace("@OLD@", "1" if os.environ.get("GEMM_AB_OLD") else "0"))
+            + HARNESS.replace("@OLD@", "1" if os.environ.get("GEMM_AB_OLD") else "0").replace("@OLDTAB@", old_table()))
     f = os.path.join(OUT, "gemm_ab.hip")
     open(f, "w").write(body)
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", f, "-o",
