@@ -701,15 +701,9 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);                   // lgkmcnt(0): this wave's LDS accesses done
   __builtin_amdgcn_s_barrier();
 }
-#ifndef G5_FW
-#define G5_FW 4               // pass F: waves per block (4: two blocks per CU)
-#endif
-#ifndef G5_FS
-#define G5_FS 2               // pass F: stages in the ring
-#endif
-#ifndef G5_FKC
-#define G5_FKC 32             // pass F: columns per stage (32: 32 KB stages; 16: 16 KB)
-#endif
+constexpr int G5_FW = 4;      // pass F: waves per block (two blocks per CU; 8 waves, one block: slower)
+constexpr int G5_FS = 2;      // pass F: stages in the ring
+constexpr int G5_FKC = 32;    // pass F: columns per stage (32 KB stages; 16 columns x 4 stages: slower)
 __host__ __device__ constexpr int g5_fstage_bytes() { return 1024 * G5_FKC; }
 
 // Pass F: one block per (shard, chunk); the chunk's 64-row tiles one after another.  NW waves
@@ -889,12 +883,8 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
 // column group w % WC (16 columns) and chain group w / WC (NCT 16-chain MFMA tiles); JB = 128
 // (default): 8 column groups x all 64 chains (4 MFMAs per A read), 48 KB stages in a 3-deep ring;
 // JB = 64: 4 column groups x 2 chain halves, 32 KB stages in a 4-deep ring (4 % slower).
-#ifndef G5_BJB
-#define G5_BJB 128
-#endif
-#ifndef G5_BNS
-#define G5_BNS 3
-#endif
+constexpr int G5_BJB = 128;   // pass B: columns per block (64: 4 % slower)
+constexpr int G5_BNS = 3;     // pass B: stages in the ring
 __host__ __device__ constexpr int g5_bstage_bytes() { return 32 * G5_BJB * 8 + 16384; }
 __global__ __launch_bounds__(64 * G5_NW, 1) void k_gemm_bwd(SweepArgs A, int njb) {
   constexpr int JB = G5_BJB, NSB = G5_BNS, WC = JB / 16, NCT = 4 * WC / G5_NW;
