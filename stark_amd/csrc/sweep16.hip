@@ -15,11 +15,12 @@
 //   DMA       16 rows of X and their y, `buffer_load_dwordx4 ... lds` (nt: X is read once per
 //             sweep) into the wave's LDS slot;
 //   forward   eta[16 rows][16 chains] on v_mfma_f64_16x16x4: k-step s, lane group lh = lane>>4
-//             takes column lh KF + s of row lane&15 (A) and beta_{lane&15} at that column (B,
-//             from the block's beta image or registers); KF = ceil(d/4) k-steps, the
+//             takes one column of row lane&15 (A) and beta_{lane&15} at that column (B, held in
+//             registers for the whole launch: no LDS reads for it); KF = ceil(d/4) k-steps, the
 //             accumulator starts at alpha;
 //   release   the backward's A operands, the last <= 4 columns and y move to registers, the
-//             slot takes the DMA of the next sub-tile;
+//             slot takes the DMA of the next sub-tile (d <= 108 logistic, every d linear; past
+//             that the slot is released after the backward: registers);
 //   residual  on the MFMA output registers (lane: rows lh + 4i, chain lane&15) -- logistic:
 //             logit_resid4 below; linear: z = (y - eta)/sigma;
 //   backward  G[16 cols][16 chains] += X_tile^T . d_eta: the D layout of the forward is the B
@@ -47,19 +48,19 @@ __host__ __device__ constexpr S16Geom s16_geom(int KF) {
   const bool VREM = REM <= 4;                   // <= 4: the VALU does the last tile
   return S16Geom{KF, JT, REM, VREM ? JT - 1 : JT, VREM};
 }
-// d > 108 (KF >= 28): the beta image no longer fits next to the slots at two workgroups per CU,
-// so beta is held in registers, and the backward's A operands (which would not fit in registers
-// beside it) are read from the slot, which is then released after the backward instead of after
-// the forward (the next DMA's latency is covered by the SIMD's other wave only).
-__host__ __device__ constexpr bool s16_breg(int KF) { return KF >= 28; }
+// Early release (PRE): the backward's A operands (4 JTM doubles) join beta (KF doubles) in
+// registers.  Logistic at KF >= 28 (d > 108) would spill, so there the backward reads them from
+// the slot, which is released after the backward (the next DMA's latency is then covered by the
+// SIMD's other wave only).  beta in registers instead of a block image in LDS: 14.00 -> 13.84 ms
+// at d = 100, 7.03 -> 6.92 ms at d = 50 linear (profiles/r04q_*).
+__host__ __device__ constexpr bool s16_pre(int FAM, int KF) { return FAM == STK_LINREG || KF <= 27; }
 constexpr int S16_FLUSH = 64;                   // sub-tiles between log1p flushes (4 elements each)
 
-template <int FAM, int KF, bool BREG = s16_breg(KF), int NACC = 2>
+template <int FAM, int KF, bool PRE = s16_pre(FAM, KF), int NACC = 2>
 __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
   constexpr S16Geom g = s16_geom(KF);
-  constexpr int C = SM_C, NW = SM_W, JTM = g.JTM, KP = 4 * KF, KB = KP + 2;
+  constexpr int C = SM_C, NW = SM_W, JTM = g.JTM;
   constexpr bool LOGI = FAM == STK_LOGREG;
-  constexpr bool PRE = !BREG;                  // early release: backward operands into registers
   const int shard = A.shard0 + blockIdx.x / A.G;
   const int chunk = blockIdx.x % A.G;
   if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
@@ -80,23 +81,15 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
 
   extern __shared__ __attribute__((aligned(16))) double lds[];
   char* const slot = reinterpret_cast<char*>(lds) + (size_t)w * SS;
-  double* const bimg = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);   // [16][KB]
-  double* const tab = bimg + (BREG ? 0 : C * KB);
+  double* const tab = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);
   double* const xst = tab + (LOGI ? EX_TAB : 0) + w * 64;      // the last tile's <= 4 columns x 16 rows
   if constexpr (LOGI) exp_table_init(tab);
   const double* qs = A.q + (size_t)shard * C * A.Dp;
-  double bf[BREG ? KF : 1];
-  if constexpr (BREG) {
+  double bf[KF];                   // beta_{lr} at the column k-step s of lane group lh takes (forward)
 #pragma unroll
-    for (int s = 0; s < KF; ++s) {
-      const int col = lh * KF + s;
-      bf[s] = col < d ? qs[(size_t)lr * A.Dp + 1 + col] : 0.0;
-    }
-  } else {
-    for (int i = tid; i < C * KP; i += NW * 64) {
-      const int c = i / KP, col = i % KP;
-      bimg[c * KB + col] = col < d ? qs[(size_t)c * A.Dp + 1 + col] : 0.0;
-    }
+  for (int s = 0; s < KF; ++s) {
+    const int col = (d & 1) ? lh * KF + s : (s < KF - (KF & 1) ? 8 * (s / 2) + 2 * lh + (s & 1) : 8 * (KF / 2) + lh);
+    bf[s] = col < d ? qs[(size_t)lr * A.Dp + 1 + col] : 0.0;
   }
   const double alpha = qs[(size_t)lr * A.Dp];
   const double inv_s = LOGI ? 0.0 : exp(-qs[(size_t)lr * A.Dp + d + 1]);
@@ -126,7 +119,10 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
   double gv[4] = {0.0, 0.0, 0.0, 0.0};
   double lm = 0.0, sp = 0.0, ll = 0.0, ga = 0.0;   // logistic lp pieces (linear: lm = sum z^2)
   const double* xs = reinterpret_cast<const double*>(slot);
-  const double* brow = bimg + lr * KB + lh * KF;
+  // column of the backward's A operand in tile t: only a last MFMA tile (no VALU remainder) can
+  // reach past d - 1 (VREM: 16 JTM = 4 KF - 4 <= d), so only it is clamped -- a clamp with the
+  // runtime d gives every (row, tile) its own address register, held across the loop
+  auto bcol = [&](int t) { return (g.VREM || t < JTM - 1) ? 16 * t + lr : std::min(16 * t + lr, d - 1); };
   const double* xrow = xs + lr * d;
 
   if (mine > 0) issue(0);
@@ -139,27 +135,26 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
     ea[0] = dbl4{alpha, alpha, alpha, alpha};
 #pragma unroll
     for (int i = 1; i < NACC; ++i) ea[i] = dbl4{0.0, 0.0, 0.0, 0.0};
-    if (!BREG && (d & 1) == 0) {
+    if ((d & 1) == 0) {
       // even d (16-B aligned rows): k-steps 2m, 2m+1 of lane group lh take columns 8m + 2 lh and
-      // 8m + 2 lh + 1, one ds_read_b128 of X and one of beta per pair instead of two ds_read_b64
-      // each (the beta image is in natural column order either way); KF odd: the last k-step
-      // takes column 8 (KF / 2) + lh.  (A/B at d = 100: 13.88 -> 13.79 ms, profiles/r04c_*)
+      // 8m + 2 lh + 1, one ds_read_b128 of X per pair instead of two ds_read_b64; KF odd: the
+      // last k-step takes column 8 (KF / 2) + lh.  (A/B at d = 100: 13.88 -> 13.79 ms,
+      // profiles/r04c_*); odd d: k-step s of lane group lh takes column lh KF + s
 #pragma unroll
       for (int m = 0; m < KF / 2; ++m) {
         const dbl2 x2 = *reinterpret_cast<const dbl2*>(xs + lr * d + 8 * m + 2 * lh);
-        const dbl2 b2 = *reinterpret_cast<const dbl2*>(bimg + lr * KB + 8 * m + 2 * lh);
-        ea[(2 * m) % NACC] = mfma_f64(x2.x, b2.x, ea[(2 * m) % NACC]);
-        ea[(2 * m + 1) % NACC] = mfma_f64(x2.y, b2.y, ea[(2 * m + 1) % NACC]);
+        ea[(2 * m) % NACC] = mfma_f64(x2.x, bf[2 * m], ea[(2 * m) % NACC]);
+        ea[(2 * m + 1) % NACC] = mfma_f64(x2.y, bf[2 * m + 1], ea[(2 * m + 1) % NACC]);
       }
       if constexpr (KF & 1) {
         const int col = 8 * (KF / 2) + lh;
-        ea[(KF - 1) % NACC] = mfma_f64(xrow[std::min(col, d - 1)], bimg[lr * KB + col], ea[(KF - 1) % NACC]);
+        ea[(KF - 1) % NACC] = mfma_f64(xrow[std::min(col, d - 1)], bf[KF - 1], ea[(KF - 1) % NACC]);
       }
     } else {
 #pragma unroll
       for (int s = 0; s < KF; ++s) {
-        const double b = BREG ? bf[s] : brow[s];
-        ea[s % NACC] = mfma_f64(xrow[std::min(lh * KF + s, d - 1)], b, ea[s % NACC]);
+        // lh KF + s <= d - 1 unless s >= KF - 3 (d >= 4 KF - 3): clamp those steps only (see bcol)
+        ea[s % NACC] = mfma_f64(xrow[s < KF - 3 ? lh * KF + s : std::min(lh * KF + s, d - 1)], bf[s], ea[s % NACC]);
       }
     }
     // ---- everything else the sub-tile needs from the slot, into registers; then release it
@@ -168,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int t = 0; t < JTM; ++t) xa[s][t] = xs[(lh + 4 * s) * d + std::min(16 * t + lr, d - 1)];
+        for (int t = 0; t < JTM; ++t) xa[s][t] = xs[(lh + 4 * s) * d + bcol(t)];
     }
     if constexpr (g.VREM) xst[lane] = xs[(lane >> 2) * d + std::min(16 * JTM + (lane & 3), d - 1)];
     uint32_t ym[4];
@@ -232,7 +227,7 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int t = 0; t < JTM; ++t)
-        gacc[t] = mfma_f64(PRE ? xa[s][t] : xs[(lh + 4 * s) * d + std::min(16 * t + lr, d - 1)], de[s], gacc[t]);
+        gacc[t] = mfma_f64(PRE ? xa[s][t] : xs[(lh + 4 * s) * d + bcol(t)], de[s], gacc[t]);
     if constexpr (g.VREM) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -313,13 +308,12 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
 
 using namespace stk;
 
-// LDS bytes of k_sweep16 at d (the main loop's slots + beta image + table + remainder scratch,
-// or the block reduction's area, whichever is larger).
+// LDS bytes of k_sweep16 at d (the main loop's slots + table + remainder scratch, or the block
+// reduction's area, whichever is larger).
 size_t stk_sweep16_lds_bytes(int family, int d) {
   const int KF = (d + 3) / 4;
   const S16Geom g = s16_geom(KF);
-  size_t main = (size_t)SM_W * sweepm_slot_bytes(d) + (s16_breg(KF) ? 0 : (size_t)SM_C * (4 * KF + 2) * 8) +
-                (family == STK_LOGREG ? EX_TAB * 8 : 0) + (size_t)SM_W * 64 * 8;
+  size_t main = (size_t)SM_W * sweepm_slot_bytes(d) + (family == STK_LOGREG ? EX_TAB * 8 : 0) + (size_t)SM_W * 64 * 8;
   const size_t red = ((size_t)SM_W * g.JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * 8;
   return std::max(main, red);
 }

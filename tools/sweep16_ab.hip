@@ -8,6 +8,10 @@
 #include "sweep_variants.hip"
 #include "../stark_amd/csrc/sweep16.hip"
 #include "sweep16_variants.hip"
+#if __has_include("_bin/s16_old.hip")
+#include "_bin/s16_old.hip"   // a committed k_sweep16 renamed k_sweep16_old (see the arms)
+#define HAVE_S16_OLD 1
+#endif
 #include "../stark_amd/csrc/datagen.hip"
 #include <stdarg.h>
 #include <stdio.h>
@@ -95,16 +99,23 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   SweepArgs A{sh_d, q, partial, nullptr, 0, C, Dp, G, LD, d + 2, 0, G, nullptr};
   const size_t l16 = stk_sweep16_lds_bytes(fam, d);
+  // LDS of the committed kernel before beta moved to registers (its block image of beta for
+  // KF < 28 beside the slots), which the legacy k_sweepe arm also fits in
+  const size_t l16_old = std::max((size_t)SM_W * sweepm_slot_bytes(d) + (size_t)16 * (4 * ((d + 3) / 4) + 2) * 8 +
+                                      (fam == STK_LOGREG ? EX_TAB * 8 : 0) + (size_t)SM_W * 64 * 8, l16);
   printf("rows/shard %lld shards %d d %d C %d family %d: G %d lds %zu / %zu, %.1f GB per sweep\n", (long long)rows, nsh,
          d, C, fam, G, lds, l16, bytes / 1e9);
   std::vector<Arm> arms;
+#ifdef HAVE_S16_OLD
+#define S16_OLD_ARM(F, KF) arms.push_back(Arm{"s16-old", (const void*)k_sweep16_old<F, KF>, l16_old, {}});
+#else
+#define S16_OLD_ARM(F, KF)
+#endif
 #define ARMS(F, KF, JT)                                                                        \
   arms = {{"s16", (const void*)k_sweep16<F, KF>, l16, {}},                                     \
-          {"e3", (const void*)k_sweepe<F, KF, JT, 0, 3, 2, 0, 2, 1>, lds, {}},                 \
-          {"x-pair", (const void*)k_sweep16x<F, KF, false, 2, false, true, 0>, l16, {}},       \
-          {"x-pb1", (const void*)k_sweep16x<F, KF, false, 2, false, true, 1>, l16, {}},        \
-          {"x-pb2", (const void*)k_sweep16x<F, KF, false, 2, false, true, 2>, l16, {}},        \
-          {"x-pb3", (const void*)k_sweep16x<F, KF, false, 2, false, true, 3>, l16, {}}};
+          {"e3", (const void*)k_sweepe<F, KF, JT, 0, 3, 2, 0, 2, 1>, l16_old, {}},                 \
+          {"late", (const void*)k_sweep16<F, KF, false>, l16, {}}};                             \
+  S16_OLD_ARM(F, KF)
   if (fam == STK_LOGREG) {
     if (d == 100) { ARMS(STK_LOGREG, 25, 7) } else { ARMS(STK_LOGREG, 13, 4) }
   } else {

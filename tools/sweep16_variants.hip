@@ -45,7 +45,7 @@ __device__ __forceinline__ double logit_resid4x(double eta, uint32_t y, const do
   return __builtin_bit_cast(double, (dvp & 0xFFFFFFFFull) | ((uint64_t)lsa31(y, (uint32_t)(dvp >> 32), LSA) << 32));   // -dv
 }
 
-template <int FAM, int KF, bool BREG = s16_breg(KF), int NACC = 2, bool LSA = false, bool PAIR = false, int PB = 0>
+template <int FAM, int KF, bool BREG = (KF >= 28), int NACC = 2, bool LSA = false, bool PAIR = false, int PB = 0>
 __global__ __launch_bounds__(256, 2) void k_sweep16x(SweepArgs A) {
   constexpr S16Geom g = s16_geom(KF);
   constexpr int C = SM_C, NW = SM_W, JTM = g.JTM, KP = 4 * KF, KB = KP + 2;
