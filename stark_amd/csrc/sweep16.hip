@@ -51,8 +51,9 @@ __host__ __device__ constexpr S16Geom s16_geom(int KF) {
 // Early release (PRE): the backward's A operands (4 JTM doubles) join beta (KF doubles) in
 // registers.  Logistic at KF >= 28 (d > 108) would spill, so there the backward reads them from
 // the slot, which is released after the backward (the next DMA's latency is then covered by the
-// SIMD's other wave only).  beta in registers instead of a block image in LDS: 14.00 -> 13.84 ms
-// at d = 100, 7.03 -> 6.92 ms at d = 50 linear (profiles/r04q_*).
+// SIMD's other wave only).  beta in registers instead of a block image in LDS: 14.00 -> 13.84 and
+// 14.24 -> 14.05 ms at d = 100 on two boxes, 7.03 -> 6.92 and 7.15 -> 7.04 ms at d = 50 linear
+// (profiles/r04q_*, r04s_*).
 __host__ __device__ constexpr bool s16_pre(int FAM, int KF) { return FAM == STK_LINREG || KF <= 27; }
 constexpr int S16_FLUSH = 64;                   // sub-tiles between log1p flushes (4 elements each)
 

@@ -44,6 +44,9 @@ def test_schools_lpgrad(ctx, orc):
                                    # > 64 sub-tiles per wave (the in-loop log1p flush of residual v4: n > 2.1e6)
                                    (500, 99, 16), (300, 113, 16), (300, 116, 16), (200, 127, 16), (64, 110, 16),
                                    (1000, 33, 16), (3000000, 4, 16), (2200000, 17, 16),
+                                   # a last MFMA tile of > 4 columns that passes d - 1 (the one clamped
+                                   # backward column, d = 94, 29, 30) and the odd-d forward's clamped last steps
+                                   (300, 94, 16), (300, 93, 16), (100, 29, 16), (100, 30, 16),
                                    # v5 two-pass fp64 MFMA GEMMs (64 chains; 70 = two batches)
                                    (1, 1, 64), (7, 3, 64), (4097, 50, 64), (333, 129, 64), (257, 300, 64),
                                    (1000, 1000, 64), (130, 1001, 70), (5000, 100, 64)])
