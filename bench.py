@@ -87,6 +87,12 @@ def parse():
     p.add_argument("--no-schools", action="store_true",
                    help="skip the configs[1] sub-record (8-schools x 4096 chains, Stan defaults; ~2 s)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "sweep_pmc.json"))
+    p.add_argument("--shard-offset", type=int, default=0,
+                   help="global id of this job's first shard: with --shards 1 --rows 1.25e7 and offset k, one rank "
+                        "of the 8-shard job (shard k's rows and RNG keys) on this GPU (tools/consensus_from_dumps.py)")
+    p.add_argument("--dump-draws", default=None,
+                   help="write this process's post-warmup draws per shard (npz: P x chains*draws, chain-major) and "
+                        "the phase times to this path")
     return p.parse_args()
 
 
@@ -184,8 +190,9 @@ def main():
     assert a.shards % world == 0, "shards must divide evenly over GPUs"
     spr = a.shards // world
     rows_per_shard = int(a.rows) // a.shards
-    first = rank * spr
+    first = a.shard_offset + rank * spr                # global id of this rank's first shard
     shard_ids = list(range(first, first + spr))
+    gather_ids = list(range(rank * spr, rank * spr + spr))  # this job's shard slots (the all-gather keys)
     ctx = engine.Context(local_rank)
 
     t = time.perf_counter()
@@ -292,9 +299,15 @@ def main():
     stats = []
     for s in range(spr):
         full = sampler.draws_device(s)
-        local[shard_ids[s]] = full.index_select(1, cols_t).contiguous()
+        local[gather_ids[s]] = full.index_select(1, cols_t).contiguous()
         stats.append(sampler.draws(s)[1][cols])
     stats = np.vstack(stats)
+    if a.dump_draws and rank == 0 and world == 1:
+        np.savez(a.dump_draws, shard_ids=np.array(shard_ids), chains=C, draws_per_chain=n_post,
+                 t_adapt=t_adapt, t_sampling=t_wsteps + elapsed + t_post, grad_evals=info["grad_evals"],
+                 leapfrogs_per_transition=float(stats[:, 3].mean()), divergent=info["divergent"],
+                 **{f"draws_{sid}": local[g].cpu().numpy() for sid, g in zip(shard_ids, gather_ids)})
+        log(f"draws of shards {shard_ids} written to {a.dump_draws}")
     t = time.perf_counter()
     allp_dev = sdist.all_gather_partitions(local, a.shards, as_tensor=True)   # one all-gather (RCCL on GPUs)
     if allp_dev.is_cuda:
@@ -345,7 +358,7 @@ def main():
         else:
             loc2, st2 = {}, []
             for s_ in range(spr):
-                loc2[shard_ids[s_]] = s2.draws_device(s_)
+                loc2[gather_ids[s_]] = s2.draws_device(s_)
                 st2.append(s2.draws(s_)[1])
             allp2 = sdist.all_gather_partitions(loc2, a.shards, as_tensor=True)
             st2 = np.vstack(st2)
