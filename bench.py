@@ -90,6 +90,9 @@ def parse():
     p.add_argument("--shard-offset", type=int, default=0,
                    help="global id of this job's first shard: with --shards 1 --rows 1.25e7 and offset k, one rank "
                         "of the 8-shard job (shard k's rows and RNG keys) on this GPU (tools/consensus_from_dumps.py)")
+    p.add_argument("--ess-budget-s", type=float, default=None,
+                   help="(one process only) stop the post-warmup phase after this many seconds and keep the draws "
+                        "every chain has by then (the line's post_warmup_draws_per_chain says how many)")
     p.add_argument("--dump-draws", default=None,
                    help="write this process's post-warmup draws per shard (npz: P x chains*draws, chain-major) and "
                         "the phase times to this path")
@@ -279,12 +282,17 @@ def main():
     # consensus pairs draw i of chain c of every shard (equal-length chains, Stan's
     # multi-chain estimator).  Its time counts in the ESS/s denominators.
     n_post = int(allreduce(np.array([max(ND, int(it1.max()) - A)], np.float64), "max")[0])
+    assert a.ess_budget_s is None or world == 1, "--ess-budget-s: one process"
     t = time.perf_counter()
     while True:                      # bounded batches with a progress line (long phases under the 2.19 criterion)
         sampler.run(A + n_post, max_steps=2000)
         its = sampler.iterations()
         log(f"ESS phase: {time.perf_counter() - t:.1f}s, post-warmup draws per chain min {its.min() - A} of {n_post}")
         if its.min() >= A + n_post:
+            break
+        if a.ess_budget_s is not None and time.perf_counter() - t > a.ess_budget_s:
+            n_post = int(its.min()) - A          # the draws every chain has: the phase ends here
+            log(f"ESS phase stopped at the {a.ess_budget_s:.0f} s budget with {n_post} post-warmup draws per chain")
             break
     ctx.sync()
     barrier()

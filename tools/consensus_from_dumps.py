@@ -55,8 +55,14 @@ def main():
             draws[int(sid)] = z[f"draws_{int(sid)}"]
         per.append({"file": os.path.basename(f), "shard_ids": [int(v) for v in z["shard_ids"]],
                     "t_adapt": float(z["t_adapt"]), "t_sampling": float(z["t_sampling"]),
+                    "draws_per_chain": int(z["draws_per_chain"]),
                     "grad_evals": int(z["grad_evals"]), "leapfrogs_per_transition": float(z["leapfrogs_per_transition"]),
                     "divergent": int(z["divergent"])})
+    # a rank stopped at a time budget (bench.py --ess-budget-s) has fewer draws per chain: the job
+    # is the first n_common draws of every chain of every rank, its wall the slowest rank's
+    ns = {k: v.shape[1] // C for k, v in draws.items()}
+    n = min(ns.values())
+    draws = {k: v.reshape(v.shape[0], C, ns[k])[:, :, :n].reshape(v.shape[0], C * n) for k, v in draws.items()}
     ids = sorted(draws)
     shards = [draws[k] for k in ids]
     comb = block_consensus(shards)
@@ -76,11 +82,14 @@ def main():
     out = {"metric": "ESS/s of the consensus, configs[3] under the reference's sampler settings, 8-GPU job run one rank "
                      "at a time on one GPU",
            "shards": ids, "chains_per_shard": C, "post_warmup_draws_per_chain": n,
+           "post_warmup_draws_per_chain_by_rank": {str(k): ns[k] for k in ids},
            "min_ess": ess, "job_wall_s": wall, "ess_per_sec": ess / wall,
            "subposterior_min_ess": {str(k): min_ess(draws[k][:-1]) for k in ids},
            "per_rank": per, "accuracy": acc,
            "posterior_mean_alpha_beta_first": [float(v) for v in comb[:4].mean(1)],
-           "note": "wall = max over ranks of (warmup + sampling) measured on one GPU per shard; consensus = "
+           "note": "wall = max over ranks of (warmup + sampling) measured on one GPU per shard (a rank stopped at a "
+                   "time budget counts to its stop); the consensus of the first post_warmup_draws_per_chain draws "
+                   "of every chain; consensus = "
                    "engine.consensus(separate_lp=True) restated in numpy; ESS = Stan 2.19's estimator "
                    "(stark_amd.diagnostics.ess), min over alpha, beta"}
     print(json.dumps(out))
