@@ -23,6 +23,7 @@ Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distribu
 """
 import argparse
 import json
+import subprocess
 import os
 import sys
 import time
@@ -86,6 +87,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-schools", action="store_true",
                    help="skip the configs[1] sub-record (8-schools x 4096 chains, Stan defaults; ~2 s)")
+    p.add_argument("--no-other-configs", action="store_true",
+                   help="skip the configs[2] / configs[4] throughput sub-records (one GPU only; ~30 s)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "sweep_pmc.json"))
     p.add_argument("--shard-offset", type=int, default=0,
                    help="global id of this job's first shard: with --shards 1 --rows 1.25e7 and offset k, one rank "
@@ -552,6 +555,33 @@ def main():
                                "after the timed window (tools/bench_schools.py)")
         except Exception as e:          # the main line is still printed
             schools = {"error": repr(e)}
+    others = None
+    if world == 1 and not dist and not a.no_other_configs:
+        # BASELINE configs[2] and configs[4] on this GPU after the timed window, throughput only
+        # (the main shards are released first: configs[4] keeps 200 GB resident)
+        model.close()
+        model = None
+        others = {}
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--family", "linear", "--rows", "1e7", "--d", "50",
+               "--adapt-iters", "150", "--ess-draws", "100", "--steps", "300", "--warmup", "20",
+               "--second-criterion", "none", "--no-cpu-baseline", "--no-schools", "--no-other-configs", "--no-accuracy"]
+        try:                            # a child process: bench.py's own line for configs[2]
+            env = {k: v for k, v in os.environ.items() if k not in ("STARK_FORCE_DIST", "RANK", "WORLD_SIZE")}
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+            l2 = json.loads(r.stdout.strip().splitlines()[-1])
+            others["configs2_linear"] = {
+                **{k: l2[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "roofline")},
+                "config": {**l2["config"], "note": "throughput sub-record: 150 warmup iterations (grads/s does not depend "
+                                                   "on it); ESS/s at Stan's 1000: profiles/r04u_bench_linear.json"},
+                "command": " ".join(["bench.py"] + cmd[2:])}
+        except Exception as e:          # the main line is still printed
+            others["configs2_linear"] = {"error": repr(e)}
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import bench_fulldata
+            others["configs4_fulldata"] = bench_fulldata.run(2.5e7, steps=10, warmup=2, seed=a.seed)
+        except Exception as e:
+            others["configs4_fulldata"] = {"error": repr(e)}
     line = {
         "metric": f"gradient evals/sec (whole node), {a.family} regression N={a.rows:.0e} d={a.d}".replace("e+0", "e"),
         "value": value,
@@ -592,6 +622,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "configs1_schools": schools,
+        "other_configs": others,
         "combine": {"gpu_ms": float(np.median(comb_ms[1:])), "gpu_ms_min": min(comb_ms[1:]),
                     "gpu_ms_first_call": comb_ms[0], "host_buffers_ms": comb_host_ms, "shards": a.shards, "P": P,
                     "draws": C * n_post, "all_gather_ms": 1e3 * t_gather,
@@ -605,7 +636,8 @@ def main():
         "divergent": info["divergent"],
     }
     print(json.dumps(line), flush=True)
-    model.close()
+    if model is not None:
+        model.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -30,52 +30,32 @@ FP64_PEAK_TFS = 78.6
 HBM_PEAK_GBS = 8000.0
 
 
-def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("--rows-per-gpu", type=float, default=2.5e7)
-    p.add_argument("--d", type=int, default=1000)
-    p.add_argument("--chains", type=int, default=64)
-    p.add_argument("--steps", type=int, default=30)
-    p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--seed", type=int, default=20240)
-    p.add_argument("--init-radius", type=float, default=2.0, help="pystan init_r (Stan default 2)")
-    p.add_argument("--nuts-criterion", choices=["stan2.19", "stan2.23"], default="stan2.19")
-    p.add_argument("--adapt-iters", type=int, default=0,
-                   help="> 0: run Stan's warmup (untimed) first and report ESS/s of the transitions the "
-                        "chains complete inside the timed window")
-    a = p.parse_args()
+def run(rows, d=1000, chains=64, steps=30, warmup=3, seed=20240, init_radius=2.0, nuts_criterion="stan2.19",
+        adapt_iters=0):
+    """One configs[4] measurement on this process's GPU (RANK / WORLD_SIZE / LOCAL_RANK from the
+    environment; the process group, if any, already initialised); returns the line (rank 0) or None."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    # STARK_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N-rank path on one
-    # GPU (ranks share devices round-robin); the driver's runs use RCCL, one rank per GPU
-    backend = os.environ.get("STARK_DIST_BACKEND", "nccl")
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
-    local_rank %= torch.cuda.device_count()
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group(backend)
+    local_rank = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
     from stark_amd import engine, fulldata
 
-    rows = int(a.rows_per_gpu)
+    rows = int(rows)
     ctx = fulldata.context_on_torch_stream(local_rank)
     t = time.perf_counter()
-    model = engine.Model.synthetic(ctx, "logistic", 1, rows, a.d, data_seed=a.seed, row_offset=rank * rows)
+    model = engine.Model.synthetic(ctx, "logistic", 1, rows, d, data_seed=seed, row_offset=rank * rows)
     ctx.sync()
     t_gen = time.perf_counter() - t
-    K, W = a.steps, a.warmup
-    A = a.adapt_iters
+    K, W = steps, warmup
+    A = adapt_iters
     nw = A if A > 0 else 1000
     total = nw + K + W + 1
-    fs = fulldata.FullDataSampler(model, num_warmup=nw, num_samples=total - nw, chains=a.chains, seed=a.seed + 1,
-                                  stepsize_jitter=0.5 if A > 0 else 0.0, init_radius=a.init_radius,
-                                  nuts_criterion=a.nuts_criterion)
+    fs = fulldata.FullDataSampler(model, num_warmup=nw, num_samples=total - nw, chains=chains, seed=seed + 1,
+                                  stepsize_jitter=0.5 if A > 0 else 0.0, init_radius=init_radius,
+                                  nuts_criterion=nuts_criterion)
     if rank == 0:
-        print(f"[bench_fulldata] {world} GPU(s) x {rows} rows x d={a.d}: {model.device_bytes() / 1e9:.1f} GB/GPU, "
+        print(f"[bench_fulldata] {world} GPU(s) x {rows} rows x d={d}: {model.device_bytes() / 1e9:.1f} GB/GPU, "
               f"generated in {t_gen:.1f}s", file=sys.stderr, flush=True)
     t_adapt = 0.0
     if A > 0:
@@ -117,7 +97,7 @@ def main():
         per = total - nw
         done = it1 - it0
         es = np.zeros(dr.shape[0] - 1)
-        for c in range(a.chains):
+        for c in range(chains):
             f0 = it0[c] - nw
             if done[c] >= 4:
                 seg = dr[:-1, c * per + f0: c * per + f0 + done[c]]
@@ -129,22 +109,22 @@ def main():
         elapsed = float(v.item())
     if min_ess:
         ess_ps = min_ess / elapsed
-    steps = i1["steps"] - i0["steps"]
+    nsteps = i1["steps"] - i0["steps"]
     grads = i1["grad_evals"] - i0["grad_evals"]      # chain-gradients of the full data set (same on every rank)
     sweeps = i1["sweeps"] - i0["sweeps"]
     avg_ms = (i1["sweep_ms"] - i0["sweep_ms"]) / max(sweeps, 1)   # qT image + pass F + pass B, this rank
-    flops = 4.0 * a.d * a.chains * rows                # two GEMMs over this rank's rows
+    flops = 4.0 * d * chains * rows                    # two GEMMs over this rank's rows
     tfs = flops / (avg_ms * 1e-3) / 1e12
-    hbm_bytes = rows * (2 * 8 * a.d + 4 + 2 * 8 * a.chains)   # X twice, y, R written + read once
+    hbm_bytes = rows * (2 * 8 * d + 4 + 2 * 8 * chains)   # X twice, y, R written + read once
     gbs = hbm_bytes / (avg_ms * 1e-3) / 1e9
     line = {
         "metric": "gradient evals/sec (whole node), full-data logistic regression d=1000, 64 chains",
         "value": grads / elapsed, "unit": "gradient evals/sec", "n_gpus": world, "steps": K, "warmup": W,
-        "ms_per_step": 1e3 * elapsed / max(steps, 1), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": 1e3 * elapsed / max(nsteps, 1), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (Philox in HBM, SURVEY 8d)",
         "config": {"workload": "full-data HMC/NUTS logistic regression, per-leapfrog gradient all-reduce",
-                   "rows_total": rows * world, "rows_per_gpu": rows, "d": a.d, "chains": a.chains,
-                   "parallelism": f"row-dp{world}", "nuts_criterion": a.nuts_criterion,
+                   "rows_total": rows * world, "rows_per_gpu": rows, "d": d, "chains": chains,
+                   "parallelism": f"row-dp{world}", "nuts_criterion": nuts_criterion,
                    "note": "N=1e9 (8 TB) exceeds node HBM; rows per GPU resident"},
         "rows_x_chains_per_sec": grads * rows * world / elapsed,
         "ess_per_sec": ess_ps, "min_ess": min_ess, "adapt_iters": A,
@@ -159,10 +139,42 @@ def main():
                              "algorithmic_bytes_per_launch": hbm_bytes}},
         "setup_s": {"datagen": t_gen, "adaptation": t_adapt},
     }
-    if rank == 0:
-        print(json.dumps(line), flush=True)
     fs.close()
     model.close()
+    return line if rank == 0 else None
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rows-per-gpu", type=float, default=2.5e7)
+    p.add_argument("--d", type=int, default=1000)
+    p.add_argument("--chains", type=int, default=64)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--seed", type=int, default=20240)
+    p.add_argument("--init-radius", type=float, default=2.0, help="pystan init_r (Stan default 2)")
+    p.add_argument("--nuts-criterion", choices=["stan2.19", "stan2.23"], default="stan2.19")
+    p.add_argument("--adapt-iters", type=int, default=0,
+                   help="> 0: run Stan's warmup (untimed) first and report ESS/s of the transitions the "
+                        "chains complete inside the timed window")
+    a = p.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # STARK_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N-rank path on one
+    # GPU (ranks share devices round-robin); the driver's runs use RCCL, one rank per GPU
+    backend = os.environ.get("STARK_DIST_BACKEND", "nccl")
+    import torch
+    import torch.distributed as dist
+    local_rank = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+    line = run(a.rows_per_gpu, a.d, a.chains, a.steps, a.warmup, a.seed, a.init_radius, a.nuts_criterion,
+               a.adapt_iters)
+    if line is not None:
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
