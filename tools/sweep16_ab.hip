@@ -107,7 +107,7 @@ int main(int argc, char** argv) {
          d, C, fam, G, lds, l16, bytes / 1e9);
   std::vector<Arm> arms;
 #ifdef HAVE_S16_OLD
-#define S16_OLD_ARM(F, KF) arms.push_back(Arm{"s16-old", (const void*)k_sweep16_old<F, KF>, l16_old, {}});
+#define S16_OLD_ARM(F, KF) arms.push_back(Arm{"s16-old", (const void*)k_sweep16_old<F, KF>, l16, {}});
 #else
 #define S16_OLD_ARM(F, KF)
 #endif
