@@ -115,7 +115,8 @@ int main(int argc, char** argv) {
   arms = {{"s16", (const void*)k_sweep16<F, KF>, l16, {}},                                     \
           {"e3", (const void*)k_sweepe<F, KF, JT, 0, 3, 2, 0, 2, 1>, l16_old, {}},                 \
           {"late", (const void*)k_sweep16<F, KF, false>, l16, {}},                              \
-          {"nacc1", (const void*)k_sweep16<F, KF, s16_pre(F, KF), 1>, l16, {}}};                \
+          {"g256", (const void*)k_sweep16<F, KF>, l16, {}, 256},                                \
+          {"g1024", (const void*)k_sweep16<F, KF>, l16, {}, 1024}};                             \
   S16_OLD_ARM(F, KF)
   if (fam == STK_LOGREG) {
     if (d == 100) { ARMS(STK_LOGREG, 25, 7) } else { ARMS(STK_LOGREG, 13, 4) }
