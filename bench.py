@@ -19,10 +19,14 @@ consensus draws / the whole sampling wall time, adaptation included (data upload
 `accuracy` compares the consensus with the full-data posterior (MAP + inverse Hessian from
 the GPU gradient, tools/laplace.py) and with the data-generating parameters.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
+Usage: python bench.py [--gpus N --steps K --warmup W].  --gpus N > 1 without a launcher starts N
+rank processes itself (one per GPU, RCCL) before any GPU call; under a
+launcher (WORLD_SIZE set) --gpus must equal the world size or the run is refused.
 """
 import argparse
+import hashlib
 import json
+import socket
 import subprocess
 import os
 import sys
@@ -43,7 +47,18 @@ FP64_MFMA4_MEASURED_TFS = 75.8  # v_mfma_f64_4x4x4_4b back to back (profiles/r02
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs = ranks (one process per GPU).  Without a launcher, N > 1 starts N rank processes "
+                        "itself; under one (torch.distributed.run), must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
+    p.add_argument("--launch-check", action="store_true",
+                   help="start the ranks, build the process group, report world size / backend / rank devices and "
+                        "exit: the launcher path without sampling (CPU: STARK_DIST_BACKEND=gloo)")
+    p.add_argument("--throughput-only", action="store_true",
+                   help="time the K steps (sampler still in adaptation) and print the line: no ESS phase, accuracy, "
+                        "second run, CPU baseline or sub-records (the chains=1 sub-record uses it)")
+    p.add_argument("--deadline-s", type=float, default=500.0,
+                   help="wall-time budget of the whole run: an optional phase (second criterion, sub-records) whose "
+                        "expected cost would cross it is skipped and the line says so")
     p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--family", choices=["logistic", "linear"], default="logistic",
@@ -69,10 +84,11 @@ def parse():
                         "(Stan >= 2.23); stan2.19: the reference's pystan 2 NUTS, whose single test lets "
                         "trajectories resonate on this near-isotropic posterior (36 vs 11 leapfrogs per "
                         "transition, DESIGN.md section 4)")
-    p.add_argument("--second-criterion", choices=["stan2.23", "stan2.19", "none"], default="stan2.19",
+    p.add_argument("--second-criterion", choices=["stan2.23", "stan2.19", "none"], default="none",
                    help="after the main run: a second adaptation + ESS phase on the same data with this "
-                        "NUTS criterion (default: the reference's pystan 2 sampler, Stan 2.19.1), reported as "
-                        "ess_second_criterion")
+                        "NUTS criterion (stan2.19: the reference's pystan 2 sampler, Stan 2.19.1), reported as "
+                        "ess_second_criterion.  Off by default since round 5: the reference sampler's own settings "
+                        "run in the configs2_linear sub-record (other_configs), where they fit the lease")
     p.add_argument("--second-jitter", type=float, default=0.5,
                    help="stepsize_jitter of the second run.  pystan 2's default is 0, under which the 2.19 "
                         "criterion's trajectories resonate on this near-isotropic posterior (profiles/r03i_bench.json: "
@@ -145,6 +161,78 @@ def cpu_combine(draws):
             "combine_note": "numpy restatement of the reference combine (lp__ in its own block), 1 process"}
 
 
+SCHOOLS_Y = [28.0, 8.0, -3.0, 7.0, -1.0, 1.0, 18.0, 12.0]        # example/stark_ex.py:5
+SCHOOLS_SIGMA = [15.0, 10.0, 16.0, 11.0, 9.0, 11.0, 10.0, 18.0]  # example/stark_ex.py:6
+
+
+def cpu_baseline_schools(seconds):
+    """The reference's CPU path for 8 schools, timed the way example/stark_ex.py:24-26 runs it:
+    pystan's single-chain NUTS (here the oracle's recursive Stan 2.19.1 twin, C) in one process
+    per run, min(runs, cores) concurrent (Spark local[*]).
+      weighted  concensusWeight(iter=5000): 2 runs of 2500 warmup + 2500 draws, one per
+                four-school partition (stark/stark.py:59-64);
+      naive     distribute(n=4): 4 full-data (J = 8) runs at iter=2000, 1000 + 1000 (the intent
+                of stark/stark.py:74-85) -- the job the configs[1] GPU record scales
+                to 4,096 chains.
+    Each job repeats with fresh seeds for about `seconds`; gradient evals/s and ESS/s (Stan 2.19
+    multi-chain ESS over the job's chains, min over mu, tau, eta, theta) per job wall time."""
+    import multiprocessing as mp
+    cores = len(os.sched_getaffinity(0))
+    ctx = mp.get_context("spawn")
+    out = {"unit": "gradient evals/sec (whole job)", "kind": "port",
+           "sample": (f"oracle orc_run_chain (recursive Stan 2.19.1 NUTS twin, C, 1 thread per run), jobs repeated "
+                      f"with fresh seeds for ~{seconds:.0f} s each; a job's wall time = its slowest run")}
+    for job, runs, J, it in (("naive_n4", 4, 8, 2000), ("weighted_iter5000", 2, 4, 5000)):
+        workers = max(1, min(runs, cores))
+        pool = ctx.Pool(workers)
+        try:
+            res = pool.starmap(_schools_worker, [(w, J, it, seconds / 2, w >= workers // 2 and J == 4)
+                                                 for w in range(workers)])
+            pool.close()
+            pool.join()
+        except BaseException:
+            pool.terminate()
+            raise
+        reps = min(len(r) for r in res)
+        walls = [max(r[k][1] for r in res) for k in range(reps)]
+        grads = [sum(r[k][0] for r in res) for k in range(reps)]
+        rec = {"runs_per_job": runs, "cores": workers, "J": J, "iter": it, "jobs_timed": reps,
+               "job_wall_ms_median": 1e3 * float(np.median(walls)),
+               "value": float(sum(grads) / sum(walls))}
+        if job == "naive_n4":
+            from stark_amd import diagnostics
+            ess = [float(np.nanmin(diagnostics.ess_matrix(np.hstack([r[k][2] for r in res]), workers)))
+                   for k in range(reps)]
+            rec["ess_per_sec"] = float(sum(ess) / sum(walls))
+            rec["min_ess_median"] = float(np.median(ess))
+        out[job] = rec
+    out["value"] = out["naive_n4"]["value"]
+    out["ess_per_sec"] = out["naive_n4"]["ess_per_sec"]
+    out["cores"] = out["naive_n4"]["cores"]
+    return out
+
+
+def _schools_worker(w, J, it, seconds, second_half):
+    """One process of a job: single-chain oracle runs on the job's data until `seconds` pass;
+    per run (gradients, seconds, P x draws of mu, tau, eta, theta)."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    lo = 4 if second_half else 0
+    y, sig = np.array(SCHOOLS_Y[lo:lo + J]), np.array(SCHOOLS_SIGMA[lo:lo + J])
+    m = O.Model(O.FAM_SCHOOLS, y=y, sigma=sig)
+    out, t_all, k = [], time.perf_counter(), 0
+    while time.perf_counter() - t_all < seconds or k < 2:
+        t = time.perf_counter()
+        r = m.run_chain(num_warmup=it // 2, num_samples=it // 2, seed=1000 + 97 * k, gid=w)
+        dt = time.perf_counter() - t
+        q = r["q"][it // 2:]
+        tau = np.exp(q[:, 1])
+        theta = q[:, :1] + tau[:, None] * q[:, 2:]
+        out.append((int(r["n_grad"]), dt, np.vstack([q[:, 0], tau, q[:, 2:].T, theta.T])))
+        k += 1
+    return out
+
+
 def _cpu_worker(d, seconds, w, family="logistic"):
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
@@ -168,10 +256,143 @@ def _cpu_worker(d, seconds, w, family="logistic"):
     return n / (time.perf_counter() - t0), rows
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` (N > 1) with no launcher around it: start N ranks, one process per GPU
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1 -- what torch.distributed.run
+    sets), and return the worst exit code.  This process never touches the GPU (torch is not even
+    imported here); rank 0 prints the line to the inherited stdout.  A rank that fails takes the
+    others down with it (they would wait in a collective).  The reference runs one partition per
+    Spark executor (stark/stark.py:65)."""
+    port = _free_port()
+    print(f"[bench] --gpus {n}: starting {n} ranks (127.0.0.1:{port})", file=sys.stderr, flush=True)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p for p in procs if p.poll() not in (None, 0)]
+            if bad:
+                rc = bad[0].returncode
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                break
+            time.sleep(0.5)
+        for p in procs:
+            p.wait()
+    except BaseException:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        raise
+    return rc or max((abs(p.returncode) for p in procs), default=0)
+
+
+def check_world(gpus, env):
+    """None when this process may run; else the reason to refuse.  `gpus` is --gpus (None: take
+    the launcher's world size), `env` the process environment."""
+    if "WORLD_SIZE" not in env:
+        return None
+    world = int(env["WORLD_SIZE"])
+    if gpus is not None and gpus != world:
+        return (f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks; a {world}-rank run "
+                f"is not reported as {gpus} GPUs")
+    return None
+
+
+def rank_devices(dist, world, rank, local_rank, dev):
+    """[[rank, local device index, PCI bus id], ...] of every rank (one all-reduce)."""
+    import torch
+    arr = np.zeros((world, 3))
+    bus = -1
+    if dev is not None:
+        bus = getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", -1)
+    arr[rank] = (rank, local_rank if dev is not None else -1, bus)
+    if dist is not None:
+        t = torch.from_numpy(arr).to(dev if dev is not None and dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t)
+        arr = t.cpu().numpy()
+    return [[int(v) for v in row] for row in arr]
+
+
+def sweep_roofline(a, rows_per_shard, sweep_ms, sweeps, shard_sweeps):
+    """The roofline object of the dominant kernel (the data sweep) from the sweep events of the
+    timed window (HIP events on the context's stream, every n-th step)."""
+    # C = 16: k_sweep16, X.[beta_1..beta_16] on fp64 MFMA (DESIGN.md 3);
+    # C <= 4: k_sweep3 (VALU), bound by HBM.
+    mfma = a.chains == 16
+    kname = "k_sweep16" if mfma else "k_sweep3"
+    ybytes = 4 if a.family == "logistic" else 8
+    fam = "LOGREG" if a.family == "logistic" else "LINREG"
+    bytes_per_shard = rows_per_shard * (8 * a.d + ybytes)   # X fp64 + y (int32 / fp64), once per sweep
+    avg_ms = sweep_ms / max(sweeps, 1)
+    shards_per_launch = shard_sweeps / max(sweeps, 1)
+    bytes_per_launch = bytes_per_shard * shards_per_launch
+    flops_per_launch = 4.0 * rows_per_shard * a.d * a.chains * shards_per_launch   # fwd + bwd GEMMs
+    gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if sweeps else None
+    tfs = flops_per_launch / (avg_ms * 1e-3) / 1e12 if sweeps else None
+    traffic = None
+    if os.path.exists(a.traffic_json):
+        try:
+            tj = json.load(open(a.traffic_json))
+            if (tj.get("kernel") == kname and tj.get("rows_per_shard") == rows_per_shard and tj.get("d") == a.d
+                    and tj.get("hbm_bytes_per_shard_sweep")):
+                # PMC pass of the same shard geometry (tools/pmc_traffic.py): FETCH_SIZE x2 per
+                # shard sweep, times the shards a launch swept on average
+                traffic = tj["hbm_bytes_per_shard_sweep"] * shards_per_launch
+        except Exception:
+            traffic = None
+    hbm = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": (gbs / HBM_PEAK_GBS) if gbs else None}
+    if mfma:
+        # arithmetic intensity 4 C d / (8 d + 4) = 7.96 flop/B at C = 16, d = 100: below the fp64
+        # machine balance (78.6 TF / 8 TB/s = 9.8 flop/B), so the roofline that bounds the sweep is
+        # HBM; the fp64-MFMA figure is reported beside it
+        intensity = flops_per_launch / bytes_per_launch
+        balance = FP64_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
+        mf = {"achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": (tfs / FP64_PEAK_TFS) if tfs else None,
+              "peak_measured": FP64_MFMA_MEASURED_TFS,
+              "peak_measured_instruction": "v_mfma_f64_16x16x4_f64 (the kernel's)",
+              "frac_of_measured": (tfs / FP64_MFMA_MEASURED_TFS) if tfs else None}
+        prim, sec, sec_name = (hbm, mf, "mfma") if intensity < balance else (mf, hbm, "hbm")
+        roof = {"bound": "hbm" if intensity < balance else "mfma", **prim, "traffic": traffic,
+                "kernel": f"{kname}<{fam}> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
+                "algorithmic_flops_per_launch": flops_per_launch, "algorithmic_bytes_per_launch": bytes_per_launch,
+                "intensity_flop_per_byte": intensity, "machine_balance_flop_per_byte": balance, sec_name: sec}
+    else:
+        roof = dict(bound="hbm", **{k: v for k, v in hbm.items()}, traffic=traffic,
+                    kernel=f"k_sweep3<{fam},{a.chains}>", avg_launch_ms=avg_ms,
+                    algorithmic_bytes_per_launch=bytes_per_launch)
+    return roof
+
+
 def main():
     a = parse()
+    refuse = check_world(a.gpus, os.environ)
+    if refuse:
+        sys.exit(refuse)
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
     if a.adapt_iters is None:
         a.adapt_iters = 150 if a.family == "logistic" else 1000
+    t_start = time.perf_counter()
+
+    def left():                        # seconds of the run's wall-time budget still unspent
+        return a.deadline_s - (time.perf_counter() - t_start)
+
+    def skipped(cost):
+        return {"skipped": f"deadline: {left():.0f} s of --deadline-s {a.deadline_s:.0f} left, this record needs ~{cost} s"}
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     # STARK_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N-rank path on one
@@ -179,17 +400,32 @@ def main():
     backend = os.environ.get("STARK_DIST_BACKEND", "nccl")
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    ndev = torch.cuda.device_count()          # counts devices without initialising the GPU
+    if backend == "nccl" and world > 1 and ndev < world:
+        sys.exit(f"bench.py: {world} ranks need {world} visible GPUs (one rank per GPU), found {ndev}; "
+                 "a rehearsal with ranks sharing a GPU: STARK_DIST_BACKEND=gloo")
     dist = None
     # STARK_FORCE_DIST=1: a process group even at world size 1 (exercises the RCCL collectives of
     # the N-rank path on one GPU: all-reduces, the draw all-gather, the Laplace gradient sums)
     if world > 1 or os.environ.get("STARK_FORCE_DIST") == "1":
         import torch.distributed as dist
-        local_rank %= torch.cuda.device_count()
-        torch.cuda.set_device(local_rank)
+        if ndev:
+            local_rank %= ndev
+            torch.cuda.set_device(local_rank)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
+    dev = local_rank if ndev else None
+    if a.launch_check:
+        devs = rank_devices(dist, world, rank, local_rank, dev)
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": world, "world_size": world,
+                              "dist_backend": dist.get_backend() if dist else None, "rank_devices": devs}), flush=True)
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     from stark_amd import dist as sdist
     from stark_amd import engine
 
@@ -238,7 +474,7 @@ def main():
     t = time.perf_counter()
     # One run to the end of warmup, in bounded step batches for progress lines: chains move
     # independently and only wait for each other once, at iteration A.
-    while True:
+    while not a.throughput_only:
         sampler.run(A, max_steps=1000)
         its = sampler.iterations()
         inf = sampler.info()
@@ -279,6 +515,26 @@ def main():
     if dist:
         elapsed = float(allreduce(np.array([elapsed]), "max")[0])
         grads, leaps = (int(v) for v in allreduce(np.array([grads, leaps], np.float64)))
+    devs = rank_devices(dist, world, rank, local_rank, dev)
+    if a.throughput_only:
+        # the timed window only (the sampler still adapting: a step costs one sweep whatever the phase)
+        roof = sweep_roofline(a, rows_per_shard, sweep_ms, sweeps, shard_sweeps)
+        sampler.close()
+        model.close()
+        if rank == 0:
+            print(json.dumps({
+                "metric": f"gradient evals/sec (whole node), {a.family} regression N={a.rows:.0e} d={a.d}".replace("e+0", "e"),
+                "value": grads / elapsed, "unit": "gradient evals/sec", "n_gpus": world, "steps": K, "warmup": W,
+                "ms_per_step": 1e3 * elapsed / K, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                "dtype": "f64", "data": "synthetic (Philox in HBM, SURVEY 8d)",
+                "config": {"workload": f"bayesian {a.family} regression, {a.shards} subposterior shards, throughput only",
+                           "rows": int(a.rows), "d": a.d, "shards": a.shards, "chains_per_shard": a.chains,
+                           "parallelism": f"shard-dp{world}"},
+                "roofline": roof, "rank_devices": devs}), flush=True)
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     # ---- ESS phase (not part of `value`): every chain of every rank runs on to the same
     # number of post-warmup draws, n_post = max(ND, the most any chain already has), so the
@@ -352,7 +608,8 @@ def main():
                 s2.run(target, max_steps=2000)
                 its = s2.iterations()
                 done = float(allreduce(np.array([float(its.min() >= target)]), "min")[0]) > 0
-                over = float(allreduce(np.array([float(time.perf_counter() - t > a.second_budget_s)]), "max")[0]) > 0
+                over = float(allreduce(np.array([float(time.perf_counter() - t > a.second_budget_s
+                                                         or left() < 150)]), "max")[0]) > 0
                 log(f"second criterion {a.second_criterion}: {time.perf_counter() - t:.1f}s, transitions per chain "
                     f"min {its.min()} of {target}")
                 if done or over:
@@ -485,51 +742,7 @@ def main():
                         "reference's joint combine (lp__ inside inv(cov), stark/stark.py:49-56). vs_fulldata_laplace: "
                         "the full-data posterior (MAP + inverse Hessian of the GPU gradient, tools/laplace.py)")
 
-    # ---- roofline of the dominant kernel (the data sweep)
-    # C = 16: k_sweep16, X.[beta_1..beta_16] on fp64 MFMA;
-    # C <= 4: k_sweep3 (VALU), bound by HBM.
-    mfma = a.chains == 16
-    kname = "k_sweep16" if mfma else "k_sweep3"
-    ybytes = 4 if a.family == "logistic" else 8
-    fam = "LOGREG" if a.family == "logistic" else "LINREG"
-    bytes_per_shard = rows_per_shard * (8 * a.d + ybytes)   # X fp64 + y (int32 / fp64), once per sweep
-    avg_ms = sweep_ms / max(sweeps, 1)
-    shards_per_launch = shard_sweeps / max(sweeps, 1)
-    bytes_per_launch = bytes_per_shard * shards_per_launch
-    flops_per_launch = 4.0 * rows_per_shard * a.d * a.chains * shards_per_launch   # fwd + bwd GEMMs
-    gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if sweeps else None
-    tfs = flops_per_launch / (avg_ms * 1e-3) / 1e12 if sweeps else None
-    traffic = None
-    if os.path.exists(a.traffic_json):
-        try:
-            tj = json.load(open(a.traffic_json))
-            if (tj.get("kernel") == kname and tj.get("rows_per_shard") == rows_per_shard and tj.get("d") == a.d
-                    and tj.get("hbm_bytes_per_shard_sweep")):
-                # PMC pass of the same shard geometry (tools/pmc_traffic.py): FETCH_SIZE x2 per
-                # shard sweep, times the shards a launch swept on average
-                traffic = tj["hbm_bytes_per_shard_sweep"] * shards_per_launch
-        except Exception:
-            traffic = None
-    hbm = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": (gbs / HBM_PEAK_GBS) if gbs else None}
-    if mfma:
-        # arithmetic intensity 4 C d / (8 d + 4) = 7.96 flop/B at C = 16, d = 100: below the fp64
-        # machine balance (78.6 TF / 8 TB/s = 9.8 flop/B), so the roofline that bounds the sweep is
-        # HBM; the fp64-MFMA figure is reported beside it
-        intensity = flops_per_launch / bytes_per_launch
-        balance = FP64_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
-        mf = {"achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": (tfs / FP64_PEAK_TFS) if tfs else None,
-              "peak_measured": FP64_MFMA_MEASURED_TFS,
-              "peak_measured_instruction": "v_mfma_f64_16x16x4_f64 (the kernel's)",
-              "frac_of_measured": (tfs / FP64_MFMA_MEASURED_TFS) if tfs else None}
-        prim, sec, sec_name = (hbm, mf, "mfma") if intensity < balance else (mf, hbm, "hbm")
-        roof = {"bound": "hbm" if intensity < balance else "mfma", **prim, "traffic": traffic,
-                "kernel": f"{kname}<{fam}> (fp64 MFMA 16x16x4, {a.chains} chains)", "avg_launch_ms": avg_ms,
-                "algorithmic_flops_per_launch": flops_per_launch, "algorithmic_bytes_per_launch": bytes_per_launch,
-                "intensity_flop_per_byte": intensity, "machine_balance_flop_per_byte": balance, sec_name: sec}
-    else:
-        roof = dict(bound="hbm", **{k: v for k, v in hbm.items()}, traffic=traffic,
-                    kernel=f"k_sweep3<{fam},{a.chains}>", avg_launch_ms=avg_ms,
-                    algorithmic_bytes_per_launch=bytes_per_launch)
+    roof = sweep_roofline(a, rows_per_shard, sweep_ms, sweeps, shard_sweeps)
     value = grads / elapsed
     # ESS per gradient evaluation of the whole run (warmup included): the same algorithm on the
     # CPU twin (transition-identical, tests/test_gpu_nuts.py) spends the same gradients per ESS
@@ -545,7 +758,7 @@ def main():
         except Exception as e:          # the GPU line is still printed
             cpu = {"error": repr(e)}
     schools = None
-    if not a.no_schools:               # BASELINE configs[1] (example/stark_ex.py 8-schools, 4096 chains), rank 0
+    if rank == 0 and not a.no_schools:  # BASELINE configs[1] (example/stark_ex.py 8-schools, 4096 chains)
         try:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             import bench_schools
@@ -553,40 +766,75 @@ def main():
             schools["note"] = ("BASELINE configs[1]: 8-schools (example/stark_ex.py data, example/schools.stan) with "
                                "4096 NUTS chains, Stan defaults (1000 warmup + 1000 draws), fused kernel; run on rank 0 "
                                "after the timed window (tools/bench_schools.py)")
+            if not a.no_cpu_baseline:
+                schools["cpu_baseline"] = (cpu_baseline_schools(a.cpu_baseline_seconds) if left() > 40
+                                           else skipped(15))
+                schools["cpu_baseline"]["note"] = (
+                    "the reference's CPU path for this data (example/stark_ex.py:24-26), one process per single-chain "
+                    "run; ess_per_sec over the whole job (warmup included): compare with ess_per_sec_whole_run")
         except Exception as e:          # the main line is still printed
             schools = {"error": repr(e)}
     others = None
     if world == 1 and not dist and not a.no_other_configs:
-        # BASELINE configs[2] and configs[4] on this GPU after the timed window, throughput only
-        # (the main shards are released first: configs[4] keeps 200 GB resident)
+        # BASELINE configs[2], configs[3] at the driver API's default chains=1, and configs[4] on
+        # this GPU after the timed window (the main shards are released first: configs[4] keeps
+        # 200 GB resident); each a child process running bench.py's own line, except configs[4]
         model.close()
         model = None
         others = {}
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--family", "linear", "--rows", "1e7", "--d", "50",
-               "--adapt-iters", "150", "--ess-draws", "100", "--steps", "300", "--warmup", "20",
-               "--second-criterion", "none", "--no-cpu-baseline", "--no-schools", "--no-other-configs", "--no-accuracy"]
-        try:                            # a child process: bench.py's own line for configs[2]
-            env = {k: v for k, v in os.environ.items() if k not in ("STARK_FORCE_DIST", "RANK", "WORLD_SIZE")}
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
-            l2 = json.loads(r.stdout.strip().splitlines()[-1])
-            others["configs2_linear"] = {
-                **{k: l2[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "roofline")},
-                "config": {**l2["config"], "note": "throughput sub-record: 150 warmup iterations (grads/s does not depend "
-                                                   "on it); ESS/s at Stan's 1000: profiles/r04u_bench_linear.json"},
-                "command": " ".join(["bench.py"] + cmd[2:])}
-        except Exception as e:          # the main line is still printed
-            others["configs2_linear"] = {"error": repr(e)}
-        try:
-            sys.path.insert(0, os.path.join(ROOT, "tools"))
-            import bench_fulldata
-            others["configs4_fulldata"] = bench_fulldata.run(2.5e7, steps=10, warmup=2, seed=a.seed)
-        except Exception as e:
-            others["configs4_fulldata"] = {"error": repr(e)}
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("STARK_FORCE_DIST", "RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+
+        def child(args, cost, keys, extra):
+            if left() < cost:
+                return skipped(cost)
+            cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
+            try:
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=max(60, left()), env=env)
+                ln = json.loads(r.stdout.strip().splitlines()[-1])
+                return {**{k: ln[k] for k in keys if k in ln}, **extra(ln), "command": " ".join(["bench.py", *args])}
+            except Exception as e:      # the main line is still printed
+                return {"error": repr(e)}
+
+        # configs[2] under pystan 2's own settings (stark/stark.py:48, 60-63): Stan 2.19.1's NUTS
+        # criterion, stepsize_jitter 0, iter = 2000 -> 1000 warmup + 1000 draws per chain
+        others["configs2_linear"] = child(
+            ["--family", "linear", "--rows", "1e7", "--d", "50", "--nuts-criterion", "stan2.19",
+             "--stepsize-jitter", "0", "--adapt-iters", "1000", "--ess-draws", "1000", "--steps", "300",
+             "--warmup", "20", "--second-criterion", "none", "--no-schools", "--no-other-configs",
+             "--cpu-baseline-seconds", str(a.cpu_baseline_seconds)] + (["--no-cpu-baseline"] if a.no_cpu_baseline else []),
+            110, ("metric", "value", "unit", "ms_per_step", "steps", "roofline", "ess_per_sec", "min_ess",
+                  "ess_per_sec_post_warmup", "leapfrogs_per_transition", "divergent", "stepsize_per_chain",
+                  "setup_s", "cpu_baseline", "config"),
+            lambda ln: {"vs_fulldata_exact": ln["accuracy"].get("vs_fulldata_exact"),
+                        "note": "the reference sampler's settings (pystan 2 = Stan 2.19.1 NUTS, stepsize_jitter 0, "
+                                "iter=2000: 1000 warmup + 1000 draws per chain, stark/stark.py:48, 60-63); ESS/s "
+                                "over the whole sampling time, warmup included"})
+        # configs[3] at the driver API's default (stark/stark.py:62-63): ONE chain per shard -> the
+        # VALU k_sweep3 (HBM-bound), throughput only
+        others["configs3_chains1"] = child(
+            ["--chains", "1", "--throughput-only", "--steps", "200", "--warmup", "10"], 40,
+            ("metric", "value", "unit", "ms_per_step", "steps", "roofline", "config"),
+            lambda ln: {"note": "concensusWeight()'s default chains=1 per partition at configs[3]'s shape (8 shards x "
+                                "1.25e7 rows, d = 100): one chain per shard, the sampler in adaptation (a step is one "
+                                "sweep whatever the phase)"})
+        if left() > 45:
+            try:
+                sys.path.insert(0, os.path.join(ROOT, "tools"))
+                import bench_fulldata
+                others["configs4_fulldata"] = bench_fulldata.run(2.5e7, steps=10, warmup=2, seed=a.seed)
+            except Exception as e:
+                others["configs4_fulldata"] = {"error": repr(e)}
+        else:
+            others["configs4_fulldata"] = skipped(45)
     line = {
         "metric": f"gradient evals/sec (whole node), {a.family} regression N={a.rows:.0e} d={a.d}".replace("e+0", "e"),
         "value": value,
         "unit": "gradient evals/sec",
         "n_gpus": world,
+        "world_size": world,
+        "dist_backend": dist.get_backend() if dist else None,
+        "rank_devices": devs,
         "steps": K,
         "warmup": W,
         "ms_per_step": 1e3 * elapsed / K,
@@ -613,7 +861,9 @@ def main():
         "num_warmup_note": (f"num_warmup = {A} (Stan's default iter=2000 would warm up for 1000; DESIGN.md 4): "
                             "the adaptation is the dominant ESS/s cost"),
         "subposterior_min_ess_shard0": ess_s0,
-        "ess_second_criterion": second_line,
+        "ess_second_criterion": second_line if second_line is not None else {
+            "note": "off by default (--second-criterion); the reference sampler's own settings (Stan 2.19.1 NUTS, "
+                    "jitter 0, 1000 + 1000) run on configs[2] in other_configs.configs2_linear"},
         "accuracy": accuracy,
         "stepsize_per_chain": {"min": float(eps.min()), "median": float(np.median(eps)), "max": float(eps.max())},
         "treedepth_mean": float(stats[:, 2].mean()),
@@ -627,6 +877,7 @@ def main():
                     "gpu_ms_first_call": comb_ms[0], "host_buffers_ms": comb_host_ms, "shards": a.shards, "P": P,
                     "draws": C * n_post, "all_gather_ms": 1e3 * t_gather,
                     "draws_on_device": bool(getattr(allp_dev, "is_cuda", False)),
+                    "consensus_sha16": hashlib.sha256(np.ascontiguousarray(comb).tobytes()).hexdigest()[:16],
                     "note": "engine.consensus(separate_lp=True) on the all-gathered draws where they lie (device "
                             "draws from RCCL: no host copy, the result left in HBM; a gloo rehearsal gathers on the "
                             "host); wall time of the call (median of 5 after the first); host_buffers_ms: the same "

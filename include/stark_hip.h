@@ -209,7 +209,10 @@ STK_API int stk_transition(stk_model* m, int shard, double* q, int32_t C, uint64
  *     (p = P, or the largest row_block block) give a rank-deficient covariance (rank <= S - 1)
  *     and raise before any arithmetic; np.linalg.inv's LU usually returns a huge finite
  *     "inverse" built from rounding noise there, and raises only on an exactly zero pivot (a
- *     constant row: both raise) -- DESIGN.md section 9;
+ *     constant row: both raise) -- DESIGN.md section 9.  An exactly duplicated parameter row
+ *     with S >> P draws is singular too: its unit-diagonal pivot is within 4.4e-16 of zero,
+ *     below P eps, so it raises; numpy raises or returns ~1e34 entries depending on the
+ *     rounding (tests/test_gpu_kernels.py::test_combine_duplicated_parameter_row_is_singular);
  *   - stk_consensus_solve takes the caller's sum W as ANY square matrix (symmetric or not) and
  *     inverts it as np.linalg.inv does, by partial pivoting, singular only on an exactly zero
  *     pivot. */

@@ -25,6 +25,8 @@ chain order (what the sampler's diagnostics need).
 """
 from __future__ import annotations
 
+import inspect
+
 import numpy as np
 
 from . import dist, engine, frontend
@@ -154,11 +156,15 @@ def sampling_config(family, datas, **kw):
         D = [len(_unconstrain(family, d, {})) for d in datas]
         cfg["init"] = np.concatenate([np.zeros(Ds * chains) for Ds in D])
     elif callable(init):
-        # pystan 2: init(chain_id=...) per chain, or init() when it takes no chain_id
+        # pystan 2: init(chain_id=...) per chain when the function takes a chain_id, else init();
+        # decided from the signature, so a TypeError raised inside the user's function propagates
+        # (chain_id = 0 .. chains - 1: parity unpinned against pystan)
         try:
-            dicts = [init(chain_id=c) for c in range(chains)]
-        except TypeError:
-            dicts = [init() for _ in range(chains)]
+            params = inspect.signature(init).parameters
+            takes_id = "chain_id" in params or any(p.kind == p.VAR_KEYWORD for p in params.values())
+        except (TypeError, ValueError):          # no introspectable signature (some builtins)
+            takes_id = False
+        dicts = [init(chain_id=c) if takes_id else init() for c in range(chains)]
         cfg["init"] = np.concatenate([_unconstrain(family, d, dicts[c]) for d in datas for c in range(chains)])
     elif isinstance(init, (list, tuple)):
         if len(init) != chains:
@@ -229,8 +235,11 @@ class Stark:
             res = model.sample(**cfg)
         finally:
             model.close()
-        self.last_run = res
         draws = [thin_draws(d, cfg["chains"], thin) for d in res.draws]
+        if thin > 1:   # last_run holds what the caller got: the thinned draws and their stats
+            idx = thin_draws(np.arange(res.chains * res.num_samples)[None, :], res.chains, thin)[0]
+            res = engine.SampleResult(draws, [st[idx] for st in res.stats], res.info, res.chains, len(idx) // res.chains)
+        self.last_run = res
         if not permuted:
             return draws
         ids = shard_ids if shard_ids is not None else range(len(datas))
@@ -272,7 +281,7 @@ class Stark:
 
         Raises stark_amd._lib.LinAlgError when a shard holds too few draws for
         its covariance to be invertible: each shard needs more than P draws, i.e.
-        (iter - warmup) * chains > P (P = the model's parameters + lp__; with separate_lp the
+        ceil((iter - warmup) / thin) * chains > P (P = the model's parameters + lp__; with separate_lp the
         parameters alone).  The reference's np.linalg.inv returns rounding noise there instead
         (DESIGN.md section 9)."""
         kwargs = self._defaults(kwargs)

@@ -225,6 +225,29 @@ def test_combine_correlated_full_rank_covariance(ctx, orc):
     np.testing.assert_allclose(out, ref, rtol=0, atol=1e-3 * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("P,i,j", [(6, 0, 1), (40, 3, 20), (102, 17, 101)])
+def test_combine_duplicated_parameter_row_is_singular(ctx, P, i, j):
+    """An exactly duplicated parameter row with S >> P draws: the sample covariance is
+    singular although S > P, so the rank bound does not catch it; the unit-diagonal matrix then
+    has a 2 x 2 block [[1, r], [r, 1]] with r within 2 ulp of 1, and the elimination's pivot for
+    the second row, 1 - r^2, lies within 4.4e-16 of zero, below the P eps threshold: LinAlgError
+    (include/stark_hip.h).  numpy's LU on the same matrix (the reference's np.linalg.inv) meets
+    either an exactly zero pivot (LinAlgError) or a rounded one and returns an 'inverse' of
+    ~1e34 entries -- which of the two depends on the rounding, so no fixture pins it."""
+    from stark_amd import engine
+    from stark_amd._lib import LinAlgError
+    rng = np.random.default_rng(P)
+    draws = []
+    for s in range(3):
+        x = rng.normal(size=(P, 4000))
+        x[j] = x[i]
+        draws.append(x + rng.normal(size=(P, 1)))
+    with pytest.raises(LinAlgError):
+        engine.consensus(draws, ctx)
+    with pytest.raises(LinAlgError):
+        engine.consensus_products(draws, ctx)
+
+
 def test_combine_device_mismatch_is_refused(ctx):
     """Device draws on another device than the context's are refused in Python, before the
     library would dereference them without peer access; the C-ABI itself stages such

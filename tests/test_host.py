@@ -109,6 +109,14 @@ def test_sampling_config_mapping():
     assert cf["init"][0] == 0.5 and cf["init"][6] == 1.5
     cg = sampling_config("schools", datas, iter=20, chains=2, seed=1, init=lambda: {"tau": 2.0})
     assert abs(cg["init"][1] - np.log(2.0)) < 1e-15 and abs(cg["init"][7] - np.log(2.0)) < 1e-15
+    # the call form comes from the signature: a TypeError raised INSIDE the user's function is
+    # the user's error, not a cue to retry without chain_id
+    def bad(chain_id):
+        raise TypeError("user bug")
+    with pytest.raises(TypeError, match="user bug"):
+        sampling_config("schools", datas, iter=20, chains=2, seed=1, init=bad)
+    ck = sampling_config("schools", datas, iter=20, chains=2, seed=1, init=lambda **kw: {"mu": kw["chain_id"] + 2.0})
+    assert ck["init"][0] == 2.0 and ck["init"][6] == 3.0
     with pytest.raises(TypeError):
         sampling_config("schools", datas, bogus=1)
 
@@ -340,3 +348,40 @@ def test_rocpd_window_selects_the_timed_dispatches(tmp_path):
     rec = json.loads(out.stdout.strip().splitlines()[-1])
     assert rec["window_dispatches"] == 3 and rec["dispatches_total"] == 5
     assert abs(rec["window_avg_ms"] - 17.0) < 1e-9
+
+
+def test_last_run_is_thinned_like_the_returned_draws(monkeypatch):
+    """thin > 1: Stark.last_run holds the draws the caller got and their per-draw stats (ADVICE
+    r4), ceil(num_samples / thin) per chain."""
+    from stark_amd import engine
+    from stark_amd import stark as S
+    from stark_amd.rdd import LocalContext
+
+    class FakeModel:
+        def __init__(self, ctx, family, shards):
+            self.n = len(shards)
+
+        def set_prior(self, **kw):
+            pass
+
+        def sample(self, **cfg):
+            C, S_ = cfg["chains"], cfg["num_samples"]
+            draws = [np.arange(19 * C * S_, dtype=float).reshape(19, C * S_) + 1000 * k for k in range(self.n)]
+            stats = [np.arange(C * S_, dtype=float)[:, None].repeat(6, 1) for _ in range(self.n)]
+            return engine.SampleResult(draws, stats, {"errors": 0}, C, S_)
+
+        def close(self):
+            pass
+
+    monkeypatch.setattr(S.engine, "Model", FakeModel)
+    monkeypatch.setattr(S.engine, "default_context", lambda *a: None)
+    sc = LocalContext()
+    school = list(zip([28, 8, -3, 7, -1, 1, 18, 12], [15, 10, 16, 11, 9, 11, 10, 18]))
+    st = S.Stark(sc, sc.parallelize(school, 2), prepare_school_data)
+    st.setStanModel(file=os.path.join(ROOT, "stark_amd", "models", "schools.stan"))
+    out = st._draw_partitions([prepare_school_data(school[:4])], iter=10, warmup=5, chains=2, thin=2, seed=3,
+                              permuted=False)
+    lr = st.last_run
+    assert out[0].shape == (19, 6) and lr.draws[0].shape == (19, 6) and lr.num_samples == 3
+    np.testing.assert_array_equal(lr.draws[0], out[0])
+    np.testing.assert_array_equal(lr.stats[0][:, 0], [0, 2, 4, 5, 7, 9])
