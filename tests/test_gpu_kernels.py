@@ -49,9 +49,18 @@ def test_schools_lpgrad(ctx, orc):
                                    (300, 94, 16), (300, 93, 16), (100, 29, 16), (100, 30, 16),
                                    # v5 two-pass fp64 MFMA GEMMs (64 chains; 70 = two batches)
                                    (1, 1, 64), (7, 3, 64), (4097, 50, 64), (333, 129, 64), (257, 300, 64),
-                                   (1000, 1000, 64), (130, 1001, 70), (5000, 100, 64)])
+                                   (1000, 1000, 64), (130, 1001, 70), (5000, 100, 64),
+                                   # pass F chunks of > 64 tiles of 64 rows (512 chunks per shard: n > 2.1e6),
+                                   # so its residual-v4 running product is flushed inside the loop too
+                                   (2200000, 5, 64)])
 @pytest.mark.parametrize("family", ["logistic", "linear"])
 def test_regression_lpgrad(ctx, orc, family, n, d, C):
+    """lp and gradient of every sweep variant vs the oracle.  Bars: lp within 1e-10 relative;
+    each gradient component within 1e-10 of max(|g_j|, 1e-3 max_j |g_j|) -- i.e. 1e-10 relative
+    for every component down to a thousandth of the largest, and 1e-13 of the largest below that.
+    The floor is there because a component that is a sum of O(n) terms of both signs cancelling
+    to near zero carries the rounding of its terms (~n eps |terms|), which no fp64 summation
+    order removes; north_star's 1e-10 relative holds for the components that do not cancel."""
     from stark_amd import engine
     rng = np.random.default_rng(n * 1000 + d)
     X = rng.uniform(-1.7, 1.7, (n, d))
@@ -82,8 +91,9 @@ def test_regression_lpgrad(ctx, orc, family, n, d, C):
 def test_logistic_lpgrad_extreme_eta(ctx, orc, scale, n, d, C):
     """|eta| from ~1 to ~1e151 (NUTS step-size probes from a dispersed init reach such points):
     Stan's +-20 cutoffs -- lt = t, dv = +-1 below, lt ~ -exp(-t) ~ 0 above -- through the
-    table-driven residuals of k_sweep16 (v4) and pass F (v3) (|t| is clamped at 700 before the
-    exp) and the VALU sweeps, vs the oracle."""
+    table-driven residual v4 of k_sweep16 and of the 64-chain pass F (k_gemm_fwd's tile epilogue;
+    |t| is clamped at 700 before the exp) and the VALU sweeps, vs the oracle.  The in-loop log1p
+    flushes of both v4 users are exercised by test_regression_lpgrad's long-chunk shapes."""
     from stark_amd import engine
     rng = np.random.default_rng(int(scale) % 1000 + n)
     X = rng.uniform(-1.7, 1.7, (n, d))

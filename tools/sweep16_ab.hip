@@ -8,6 +8,7 @@
 #include "sweep_variants.hip"
 #include "../stark_amd/csrc/sweep16.hip"
 #include "sweep16_variants.hip"
+#include "sweep16_r5.hip"
 #if __has_include("_bin/s16_old.hip")
 #include "_bin/s16_old.hip"   // a committed k_sweep16 renamed k_sweep16_old (see the arms)
 #define HAVE_S16_OLD 1
@@ -113,10 +114,12 @@ int main(int argc, char** argv) {
 #endif
 #define ARMS(F, KF, JT)                                                                        \
   arms = {{"s16", (const void*)k_sweep16<F, KF>, l16, {}},                                     \
-          {"e3", (const void*)k_sweepe<F, KF, JT, 0, 3, 2, 0, 2, 1>, l16_old, {}},                 \
-          {"late", (const void*)k_sweep16<F, KF, false>, l16, {}},                              \
-          {"g256", (const void*)k_sweep16<F, KF>, l16, {}, 256},                                \
-          {"g1024", (const void*)k_sweep16<F, KF>, l16, {}, 1024}};                             \
+          {"v0", (const void*)k_sweep16v<F, KF, 0>, l16, {}},                                  \
+          {"dppv", (const void*)k_sweep16v<F, KF, 64>, l16, {}},                               \
+          {"fpd2", (const void*)k_sweep16v<F, KF, 512>, l16, {}},                              \
+          {"fpd3", (const void*)k_sweep16v<F, KF, 768>, l16, {}},                              \
+          {"dppv-fpd2", (const void*)k_sweep16v<F, KF, 576>, l16, {}},                         \
+          {"dppv-peel", (const void*)k_sweep16v<F, KF, 96>, l16, {}}};                         \
   S16_OLD_ARM(F, KF)
   if (fam == STK_LOGREG) {
     if (d == 100) { ARMS(STK_LOGREG, 25, 7) } else { ARMS(STK_LOGREG, 13, 4) }
