@@ -38,6 +38,35 @@ def ablation_copy(src):
     return "namespace stk {\n" + k + "\n}  // namespace stk\n"
 
 
+def deferred_copy(src):
+    """k_gemm_fwd_d<FAM>: the product pass F with the tile's R stores issued at the top of the
+    next stage (after its barrier and DMA issue) instead of at the tile's end followed by
+    vmcnt(0): the stores' write latency then runs under the next stage's MFMAs and is waited for
+    by the following stage's vmcnt(0) (NS = 2: every stage waits for vmcnt(0) anyway)."""
+    i = src.index("template <int FAM>\n__global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A) {")
+    j = src.index("\n}\n", i) + 3
+    k = src[i:j].replace("void k_gemm_fwd(SweepArgs A) {", "void k_gemm_fwd_d(SweepArgs A) {")
+    old_loop = "  for (int st = 0; st < nst; ++st) {\n    const int kc = st % NKC;\n"
+    assert k.count(old_loop) == 1
+    k = k.replace(old_loop, "  double rdv[NCT][4];\n  int rtile = -1;\n"
+                  "  auto flush_r = [&]() {\n#pragma unroll\n    for (int c2 = 0; c2 < NCT; ++c2)\n#pragma unroll\n"
+                  "      for (int i = 0; i < 4; ++i)\n        *reinterpret_cast<double*>(Rimg + g5_chain_off(rtile * G5_TR + 16 * wr + lh + 4 * i, "
+                  "16 * (NCT * wc + c2) + lr)) = rdv[c2][i];\n  };\n" + old_loop)
+    old_issue = "    if (st + NS - 1 < nst) issue(st + NS - 1);\n"
+    assert k.count(old_issue) == 1
+    k = k.replace(old_issue, old_issue + "    if (kc == 0 && st > 0) flush_r();               // the previous tile's R rows\n")
+    old_store = "          *reinterpret_cast<double*>(Rimg + g5_chain_off((int)grow, 16 * ct + lr)) = dv;\n"
+    assert k.count(old_store) == 1
+    k = k.replace(old_store, "          rdv[c2][i] = dv;\n")
+    old_wait = "      __builtin_amdgcn_s_waitcnt(0xF70);                  // vmcnt(0): R stores retired before the next counted DMA wait\n"
+    assert k.count(old_wait) == 1
+    k = k.replace(old_wait, "      rtile = tile;\n")
+    old_end = "  double lpa[NCT];\n"
+    assert k.count(old_end) == 1
+    k = k.replace(old_end, "  if (rtile >= 0) flush_r();\n" + old_end, 1)
+    return "namespace stk {\n" + k + "\n}  // namespace stk\n"
+
+
 HARNESS = r'''
 #include <stdarg.h>
 #include <stdio.h>
@@ -88,9 +117,12 @@ int main(int argc, char** argv) {
 #if HAVE_OLD
   arms.push_back(Arm{"F-old", (const void*)k_gemm_fwd_old<STK_LOGREG>, 0, lds_old, true, {}});
 #endif
-  arms.push_back(Arm{"F-r1k32s2", gemm_fwd_t_ptr<2, 32, 1>(), 0, gemm_fwd_t_lds<2, 32, 1>(), true, {}});
-  arms.push_back(Arm{"F-r2k16s2", gemm_fwd_t_ptr<2, 16, 2>(), 0, gemm_fwd_t_lds<2, 16, 2>(), true, {}});
-  arms.push_back(Arm{"F-r2k16s3", gemm_fwd_t_ptr<3, 16, 2>(), 0, gemm_fwd_t_lds<3, 16, 2>(), true, {}});
+  arms.push_back(Arm{"F-defer", (const void*)k_gemm_fwd_d<STK_LOGREG>, 0, lds, true, {}});
+  if (getenv("GEMM_AB_TILES")) {
+    arms.push_back(Arm{"F-r1k32s2", gemm_fwd_t_ptr<2, 32, 1>(), 0, gemm_fwd_t_lds<2, 32, 1>(), true, {}});
+    arms.push_back(Arm{"F-r2k16s2", gemm_fwd_t_ptr<2, 16, 2>(), 0, gemm_fwd_t_lds<2, 16, 2>(), true, {}});
+    arms.push_back(Arm{"F-r2k16s3", gemm_fwd_t_ptr<3, 16, 2>(), 0, gemm_fwd_t_lds<3, 16, 2>(), true, {}});
+  }
   if (getenv("GEMM_AB_ABL")) {
     arms.push_back(Arm{"F-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 1>, 0, lds, false, {}});
     arms.push_back(Arm{"F-noEpi", (const void*)k_gemm_fwd_x<STK_LOGREG, 4>, 0, lds, false, {}});
@@ -171,7 +203,7 @@ def main():
     body = ('#include "%s"\n#include "%s"\n#include "%s"\n' % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"),
                                                           os.path.join(c, "datagen.hip"))
             + '#include "%s"\n#include "%s"\n' % (os.path.join(ROOT, "tools", "sweep_legacy.hip"), os.path.join(ROOT, "tools", "gemm_fwd_variants.hip"))
-            + ablation_copy(src) + (old_copy(os.environ.get("GEMM_AB_OLD", "HEAD")) if os.environ.get("GEMM_AB_OLD") else "")
+            + ablation_copy(src) + deferred_copy(src) + (old_copy(os.environ.get("GEMM_AB_OLD", "HEAD")) if os.environ.get("GEMM_AB_OLD") else "")
             + HARNESS.replace("@OLD@", "1" if os.environ.get("GEMM_AB_OLD") else "0").replace("@OLDTAB@", old_table()))
     f = os.path.join(OUT, "gemm_ab.hip")
     open(f, "w").write(body)
