@@ -117,7 +117,9 @@ int main(int argc, char** argv) {
 #if HAVE_OLD
   arms.push_back(Arm{"F-old", (const void*)k_gemm_fwd_old<STK_LOGREG>, 0, lds_old, true, {}});
 #endif
-  arms.push_back(Arm{"F-defer", (const void*)k_gemm_fwd_d<STK_LOGREG>, 0, lds, true, {}});
+  if (getenv("GEMM_AB_DEFER")) arms.push_back(Arm{"F-defer", (const void*)k_gemm_fwd_d<STK_LOGREG>, 0, lds, true, {}});
+  arms.push_back(Arm{"F8-s2", (const void*)k_gemm_fwd8<STK_LOGREG, 2>, 2, gemm_fwd8_lds<STK_LOGREG, 2>(), true, {}});
+  arms.push_back(Arm{"F8-s3", (const void*)k_gemm_fwd8<STK_LOGREG, 3>, 2, gemm_fwd8_lds<STK_LOGREG, 3>(), true, {}});
   if (getenv("GEMM_AB_TILES")) {
     arms.push_back(Arm{"F-r1k32s2", gemm_fwd_t_ptr<2, 32, 1>(), 0, gemm_fwd_t_lds<2, 32, 1>(), true, {}});
     arms.push_back(Arm{"F-r2k16s2", gemm_fwd_t_ptr<2, 16, 2>(), 0, gemm_fwd_t_lds<2, 16, 2>(), true, {}});
@@ -133,6 +135,7 @@ int main(int argc, char** argv) {
   const int njb = (d + G5_BJB - 1) / G5_BJB;
   auto launch = [&](const Arm& a) {
     if (a.kind == 0) hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.k)), dim3(nsh * G), dim3(64 * G5_FW), a.lds, st, A);
+    else if (a.kind == 2) hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.k)), dim3(nsh * G), dim3(512), a.lds, st, A);
     else hipLaunchKernelGGL(k_gemm_bwd, dim3(nsh * G * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
   };
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -202,7 +205,8 @@ def main():
     c = os.path.join(ROOT, "stark_amd", "csrc")
     body = ('#include "%s"\n#include "%s"\n#include "%s"\n' % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"),
                                                           os.path.join(c, "datagen.hip"))
-            + '#include "%s"\n#include "%s"\n' % (os.path.join(ROOT, "tools", "sweep_legacy.hip"), os.path.join(ROOT, "tools", "gemm_fwd_variants.hip"))
+            + '#include "%s"\n#include "%s"\n#include "%s"\n' % (os.path.join(ROOT, "tools", "sweep_legacy.hip"), os.path.join(ROOT, "tools", "gemm_fwd_variants.hip"),
+                                                  os.path.join(ROOT, "tools", "gemm_fwd_r5.hip"))
             + ablation_copy(src) + deferred_copy(src) + (old_copy(os.environ.get("GEMM_AB_OLD", "HEAD")) if os.environ.get("GEMM_AB_OLD") else "")
             + HARNESS.replace("@OLD@", "1" if os.environ.get("GEMM_AB_OLD") else "0").replace("@OLDTAB@", old_table()))
     f = os.path.join(OUT, "gemm_ab.hip")

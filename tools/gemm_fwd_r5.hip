@@ -1,0 +1,168 @@
+// Round-5 measurement variant of pass F (stark_amd/csrc/sweep.hip: k_gemm_fwd) for
+// tools/gemm_fwd_ab.py: 128-row tiles shared by 8 waves (one block per CU, two waves per SIMD),
+// each wave 16 rows x all 64 chains -- the product's per-wave shape -- so one beta^T stage feeds
+// twice the rows: the LDS-DMA volume per row drops from 2 x (X) to 1.5 x (X) (the product's two
+// 4-wave blocks per CU each re-stream all of beta^T per 64 rows), and NS stages of 48 KB give a
+// deeper prefetch.  Chunk row ranges stay those of 64-row tiles (pass B, the reduction and the
+// placement independence are unchanged): a chunk's last 128-row tile may be half empty, and no R
+// row past the chunk's 64-row-aligned end is written.
+// Included after sweep.hip (namespace stk).
+namespace stk {
+
+template <int FAM, int NS>
+__global__ __launch_bounds__(512, 1) void k_gemm_fwd8(SweepArgs A) {
+  constexpr int NW = 8, NCT = 4, TR = 128;
+  constexpr int KCF = 32, XB = TR * KCF * 8, BB = KCF * 512, STG = XB + BB;   // stage: [X 128 x KCF][beta^T KCF x 64]
+  constexpr int PPR = KCF / 2;                          // 16-B pieces per X row in the stage
+  constexpr int NDX = XB / 1024 / NW, NDB = BB / 1024 / NW;
+  static_assert(NDX >= 1 && NDB >= 1, "pass F8 stage geometry");
+  auto swz = [](int row) { return row & 15; };
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d, KP = g5_kp(d), NKC = KP / KCF;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;       // the chunk geometry of 64-row tiles
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * G5_TR, r1 = std::min<int64_t>(sh.n, t1 * G5_TR);
+  const int nrows = (int)(r1 - r0);
+  const int rcap = (int)((t1 - t0) * G5_TR);           // R rows of this chunk
+  const int ntile = (rcap + TR - 1) / TR;
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const stg = reinterpret_cast<char*>(lds);
+  double* const sptab = reinterpret_cast<double*>(stg + NS * STG);
+  if constexpr (FAM == STK_LOGREG) exp_table_init(sptab);
+  const double* qb = A.q + (size_t)shard * G5_C * A.Dp;
+  double alpha[NCT], inv_s[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) {
+    alpha[c2] = qb[(size_t)(16 * c2 + lr) * A.Dp];
+    inv_s[c2] = (FAM == STK_LINREG) ? exp(-qb[(size_t)(16 * c2 + lr) * A.Dp + d + 1]) : 0.0;
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0xF70);
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
+  const __amdgpu_buffer_rsrc_t br = uniform_rsrc(A.qT + (size_t)shard * KP * G5_C, (int64_t)KP * G5_C * 8);
+  int xvo[NDX];
+#pragma unroll
+  for (int i = 0; i < NDX; ++i) {
+    const int sl = (w * NDX + i) * 64 + lane, row = sl / PPR, pc = (sl % PPR) ^ swz(row);
+    xvo[i] = row * d * 8 + pc * 16;
+  }
+  auto issue = [&](int st) {
+    const int tile = st / NKC, kc = st % NKC;
+    char* b = stg + (st % NS) * STG;
+    const int xso = tile * TR * d * 8 + kc * KCF * 8;
+#pragma unroll
+    for (int i = 0; i < NDX; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * NDX + i) * 1024), 16, xvo[i], xso, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NDB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(br, (lds_vptr)(b + XB + (w * NDB + i) * 1024), 16, lane * 16,
+                                               kc * KCF * 512 + (w * NDB + i) * 1024, 0, 0);
+  };
+  double lm[NCT], sp[NCT], ll[NCT], gaa[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) lm[c2] = sp[c2] = ll[c2] = gaa[c2] = 0.0;
+  char* const Rimg = reinterpret_cast<char*>(A.R + ((size_t)shard * A.Rrows + r0) * G5_C);
+  const int nst = ntile * NKC;
+  for (int s0 = 0; s0 < NS - 1 && s0 < nst; ++s0) issue(s0);
+  dbl4 acc[NCT];
+  double yt[4] = {0.0, 0.0, 0.0, 0.0};
+  uint32_t yit[4] = {0u, 0u, 0u, 0u};
+  for (int st = 0; st < nst; ++st) {
+    const int kc = st % NKC;
+    if (kc == 0) {
+#pragma unroll
+      for (int c2 = 0; c2 < NCT; ++c2) acc[c2] = dbl4{0.0, 0.0, 0.0, 0.0};
+    }
+    // own DMAs of stage st retired: the stages after it (at most NS - 2) may stay in flight; a
+    // stricter wait also covers the tile's y loads issued one stage earlier
+    wait_vmcnt(std::min(NS - 2, nst - 1 - st) * (NDX + NDB));
+    lds_barrier();
+    if (st + NS - 1 < nst) issue(st + NS - 1);
+    if (kc == (NKC > 1 ? 1 : 0)) {                       // the tile's y, a stage ahead of its epilogue
+      const int64_t tb = (int64_t)(st / NKC) * TR + 16 * w + lh;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t grow = tb + 4 * i;
+        if constexpr (FAM == STK_LOGREG) yit[i] = grow < nrows ? (uint32_t)sh.yi[r0 + grow] : 0u;
+        else yt[i] = grow < nrows ? sh.y[r0 + grow] : 0.0;
+      }
+    }
+    const char* b = stg + (st % NS) * STG;
+    const int r = 16 * w + lr;
+#pragma unroll
+    for (int step = 0; step < KCF / 4; ++step) {
+      const int kk = 4 * step + lh;
+      const double a = *reinterpret_cast<const double*>(b + r * (16 * PPR) + (((kk >> 1) ^ swz(r)) << 4) + ((kk & 1) << 3));
+#pragma unroll
+      for (int c2 = 0; c2 < NCT; ++c2)
+        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + XB + g5_chain_off(kk, 16 * c2 + lr)), acc[c2]);
+    }
+    if (kc == NKC - 1) {
+      const int tile = st / NKC;
+#pragma unroll
+      for (int c2 = 0; c2 < NCT; ++c2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 16 * w + lh + 4 * i;
+          const int grow = tile * TR + row;
+          const bool valid = grow < nrows;
+          const double eta = acc[c2][i] + alpha[c2];
+          double dv;
+          if constexpr (FAM == STK_LOGREG) {
+            double lm2 = lm[c2], sp2 = sp[c2];
+            dv = -logit_resid4(eta, yit[i], sptab, lm2, sp2);
+            lm[c2] = valid ? lm2 : lm[c2];
+            sp[c2] = valid ? sp2 : sp[c2];
+          } else {
+            const double z = (yt[i] - eta) * inv_s[c2];
+            lm[c2] += valid ? z * z : 0.0;
+            dv = z * inv_s[c2];
+          }
+          dv = valid ? dv : 0.0;
+          gaa[c2] += dv;
+          if (grow < rcap) *reinterpret_cast<double*>(Rimg + g5_chain_off(grow, 16 * c2 + lr)) = dv;
+        }
+      }
+      if constexpr (FAM == STK_LOGREG) {
+        if ((tile & 31) == 31) {                          // 32 tiles x 4 rows = 128 elements per lane
+#pragma unroll
+          for (int c2 = 0; c2 < NCT; ++c2) {
+            ll[c2] += log1p(sp[c2]);
+            sp[c2] = 0.0;
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xF70);                  // vmcnt(0): R stores retired before the next counted wait
+    }
+  }
+  double lpa[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] = (FAM == STK_LOGREG) ? 0.5 * lm[c2] - (ll[c2] + log1p(sp[c2])) : lm[c2];
+  __syncthreads();
+  double* red = lds;                                     // [NW waves][64 lanes][NCT][2]
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) {
+    red[((w * 64 + lane) * NCT + c2) * 2 + 0] = lpa[c2];
+    red[((w * 64 + lane) * NCT + c2) * 2 + 1] = gaa[c2];
+  }
+  __syncthreads();
+  if (tid < 2 * G5_C) {
+    const int c = tid >> 1, kind = tid & 1, c2 = c >> 4, l = c & 15;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww)
+      for (int h = 0; h < 4; ++h) v += red[((ww * 64 + h * 16 + l) * NCT + c2) * 2 + kind];
+    A.partial[(((size_t)shard * A.Gs + chunk) * G5_C + c) * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
+}
+
+template <int FAM, int NS>
+constexpr size_t gemm_fwd8_lds() { return (size_t)NS * (128 * 32 * 8 + 32 * 512) + EX_TAB * 8; }
+
+}  // namespace stk
