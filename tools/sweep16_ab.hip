@@ -115,11 +115,9 @@ int main(int argc, char** argv) {
 #define ARMS(F, KF, JT)                                                                        \
   arms = {{"s16", (const void*)k_sweep16<F, KF>, l16, {}},                                     \
           {"v0", (const void*)k_sweep16v<F, KF, 0>, l16, {}},                                  \
-          {"dppv", (const void*)k_sweep16v<F, KF, 64>, l16, {}},                               \
-          {"fpd2", (const void*)k_sweep16v<F, KF, 512>, l16, {}},                              \
-          {"fpd3", (const void*)k_sweep16v<F, KF, 768>, l16, {}},                              \
-          {"dppv-fpd2", (const void*)k_sweep16v<F, KF, 576>, l16, {}},                         \
-          {"dppv-peel", (const void*)k_sweep16v<F, KF, 96>, l16, {}}};                         \
+          {"dppv2", (const void*)k_sweep16v<F, KF, 128>, l16, {}},                             \
+          {"dppv2-peel", (const void*)k_sweep16v<F, KF, 160>, l16, {}},                        \
+          {"dppv", (const void*)k_sweep16v<F, KF, 64>, l16, {}}};                              \
   S16_OLD_ARM(F, KF)
   if (fam == STK_LOGREG) {
     if (d == 100) { ARMS(STK_LOGREG, 25, 7) } else { ARMS(STK_LOGREG, 13, 4) }

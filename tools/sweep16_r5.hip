@@ -13,6 +13,8 @@
 //  64  DPPV    the VALU last tile's X values as 4 registers per lane read from the slot before
 //              the release (lane lr & 3 of each row), broadcast by v_fmac_f64_dpp row_newbcast:
 //              no LDS copy and 2 KB instead of 8 KB of LDS reads per sub-tile
+// 128  DPPV2   the same from ONE register per lane: X[lh + 4 (lr >> 2)][16 JTM + (lr & 3)], so the
+//              value of (row lh + 4i, column jj) is lane 4i + jj of the DPP row: 512 B of LDS reads
 // 256 x FPD    the forward's X pairs read FPD pairs ahead of their MFMAs
 // Included after sweep16.hip (namespace stk).
 namespace stk {
@@ -21,6 +23,7 @@ template <int FAM, int KF, int V, bool PRE = s16_pre(FAM, KF), int NACC = 2>
 __global__ __launch_bounds__(256, 2) void k_sweep16v(SweepArgs A) {
   constexpr bool NOWAIT = V & 1, NORES = V & 2, NOXA = V & 4, NOVREM = V & 8, EARLYXA = V & 16, PEEL = V & 32;
   constexpr bool DPPV = V & 64;                 // VALU last tile from a DPP broadcast (no LDS copy)
+  constexpr bool DPPV2 = V & 128;               // ... from ONE register per lane (row lh + 4 (lr >> 2), column lr & 3)
   constexpr int FPD = (V >> 8) & 7;             // forward read-ahead depth in X pairs (0: the compiler's)
   constexpr S16Geom g = s16_geom(KF);
   constexpr bool VREM = g.VREM && !NOVREM;
@@ -150,7 +153,10 @@ __global__ __launch_bounds__(256, 2) void k_sweep16v(SweepArgs A) {
         for (int t = 0; t < JTM; ++t) xa[s][t] = NOXA ? 1e-3 * (lane + 7 * s + 3 * t) : xs[(lh + 4 * s) * d + bcol(t)];
     }
     double xv[4];
-    if constexpr (VREM && DPPV) {   // lane (lr, lh): X[lh + 4i][16 JTM + (lr & 3)]; lanes lr = 0..3 are broadcast
+    double xv2 = 0.0;
+    if constexpr (VREM && DPPV2) {
+      xv2 = xs[(lh + 4 * (lr >> 2)) * d + std::min(16 * JTM + (lr & 3), d - 1)];
+    } else if constexpr (VREM && DPPV) {   // lane (lr, lh): X[lh + 4i][16 JTM + (lr & 3)]; lanes lr = 0..3 are broadcast
 #pragma unroll
       for (int i = 0; i < 4; ++i) xv[i] = xs[(lh + 4 * i) * d + std::min(16 * JTM + (lr & 3), d - 1)];
     } else if constexpr (VREM) {
@@ -221,7 +227,19 @@ __global__ __launch_bounds__(256, 2) void k_sweep16v(SweepArgs A) {
 #pragma unroll
       for (int t = 0; t < JTM; ++t)
         gacc[t] = mfma_f64(PRE ? xa[s][t] : xs[(lh + 4 * s) * d + bcol(t)], de[s], gacc[t]);
-    if constexpr (VREM && DPPV) {
+    if constexpr (VREM && DPPV2) {
+      // gv[jj] += X[lh + 4i][16 JTM + jj] * de[i]: that X value sits in lane 4i + jj of this lane's
+      // DPP row (rows lh + 4i of every chain share the row), broadcast by row_newbcast
+#define S16_F(I, J, G) "v_fmac_f64_dpp %" #G ", %4, %" #I " row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"
+      asm volatile("s_nop 1\n\t"
+                   S16_F(5, 0, 0) S16_F(5, 1, 1) S16_F(5, 2, 2) S16_F(5, 3, 3)
+                   S16_F(6, 4, 0) S16_F(6, 5, 1) S16_F(6, 6, 2) S16_F(6, 7, 3)
+                   S16_F(7, 8, 0) S16_F(7, 9, 1) S16_F(7, 10, 2) S16_F(7, 11, 3)
+                   S16_F(8, 12, 0) S16_F(8, 13, 1) S16_F(8, 14, 2) S16_F(8, 15, 3)
+                   : "+v"(gv[0]), "+v"(gv[1]), "+v"(gv[2]), "+v"(gv[3])
+                   : "v"(xv2), "v"(de[0]), "v"(de[1]), "v"(de[2]), "v"(de[3]));
+#undef S16_F
+    } else if constexpr (VREM && DPPV) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {   // gv[jj] += X[lh + 4i][16 JTM + jj] (lane jj of the row) * de[i]
         // s_nop 1: two wait states between any VALU write of %4 (a copy the register allocator
