@@ -731,11 +731,15 @@ struct NutsChain {
       c_g[k] = g[k];
       c_pb[k] = p[k];
     }
-    if (IV(I_DIV)) return end_transition(pause_at);
+    // every way out that ends the transition leaves through ONE end_transition call after the
+    // tree code (a divergent leaf, a U-turn inside a merge, the top level): an inlined call
+    // inside the merge loop made the loop body carry end_transition's code and registers (27
+    // register copies and the structurizer's mask juggling per merge in the fused kernel's ISA)
+    bool stop = IV(I_DIV) != 0;
     const int depth = IV(I_DEPTH);
     const int n = IV(I_LEAF);
     int j = 0;
-    while (j < depth && ((n >> j) & 1)) {
+    while (!stop && j < depth && ((n >> j) & 1)) {
       // merge pending left sub-tree (level j) with the just-completed right one
       const double l_lsw = stks[j * SS_COUNT + SS_LSW];
       double l_rho[NCH], l_psb[NCH];
@@ -798,10 +802,10 @@ struct NutsChain {
       }
       c_lsw = lsw_sub;
       const bool ok1 = criterion(l_psb, c_pse, c_rho);
-      if (!ok1 || !junction_ok) return end_transition(pause_at);
+      stop = !ok1 || !junction_ok;
       ++j;
     }
-    if (j < depth) {
+    if (!stop && j < depth) {
       // push the completed sub-tree as the pending left sub-tree of level j
       st(svp(j, SV_RHO), c_rho);
       st(svp(j, SV_PSB), c_psb);
@@ -819,99 +823,103 @@ struct NutsChain {
       begin_leapfrog(IV(I_DIR) * S(S_EPS));
       return true;
     }
-    // the top-level sub-tree of this depth is complete and valid
-    const int fwd = IV(I_DIR) > 0;
-    double o_p[NCH], o_ps[NCH];     // the old trajectory's end next to the new sub-tree
-    if (uext()) {
-      ld(vp(fwd ? V_PF : V_PB), o_p);
-      ld(vp(fwd ? V_PSP : V_PSM), o_ps);
-    }
-    st(vp(fwd ? V_QF : V_QB), q);
-    st(vp(fwd ? V_PF : V_PB), p);
-    st(vp(fwd ? V_GF : V_GB), g);
-    // (no run-time index into the register arrays: that would move them to scratch)
-    S(S_VF) = fwd ? S(S_V) : S(S_VF);
-    S(S_VB) = fwd ? S(S_VB) : S(S_V);
-    IV(I_DEPTH) = depth + 1;
-    const double u = uniform();
-    bool take;
-    double lsw_new;
-    if constexpr (FM) {   // one exp for both: e = exp(-|c_lsw - lsw|) is exp(c_lsw - lsw) when c_lsw <= lsw
-      double e;
-      lsw_new = log_sum_exp_mt_e(S(S_LSW), c_lsw, mt, e);
-      take = c_lsw > S(S_LSW) || u < e;
-    } else {
-      take = c_lsw > S(S_LSW) || u < ex(c_lsw - S(S_LSW));
-      lsw_new = lse(S(S_LSW), c_lsw);
-    }
-    double rho[NCH], psp[NCH], psm[NCH], rho_old[NCH];
-    if constexpr (FM) {   // branch-free: the sample point rewritten with a select (LDS image)
-      double o_q[NCH], o_g[NCH], nq[NCH], ng[NCH];
-      ld(vp(V_QS), o_q);
-      ld(vp(V_GS), o_g);
-      ld(vp(V_RHO), rho);
+    if (!stop) {
+      // the top-level sub-tree of this depth is complete and valid
+      const int fwd = IV(I_DIR) > 0;
+      double o_p[NCH], o_ps[NCH];     // the old trajectory's end next to the new sub-tree
+      if (uext()) {
+        ld(vp(fwd ? V_PF : V_PB), o_p);
+        ld(vp(fwd ? V_PSP : V_PSM), o_ps);
+      }
+      st(vp(fwd ? V_QF : V_QB), q);
+      st(vp(fwd ? V_PF : V_PB), p);
+      st(vp(fwd ? V_GF : V_GB), g);
+      // (no run-time index into the register arrays: that would move them to scratch)
+      S(S_VF) = fwd ? S(S_V) : S(S_VF);
+      S(S_VB) = fwd ? S(S_VB) : S(S_V);
+      IV(I_DEPTH) = depth + 1;
+      const double u = uniform();
+      bool take;
+      double lsw_new;
+      if constexpr (FM) {   // one exp for both: e = exp(-|c_lsw - lsw|) is exp(c_lsw - lsw) when c_lsw <= lsw
+        double e;
+        lsw_new = log_sum_exp_mt_e(S(S_LSW), c_lsw, mt, e);
+        take = c_lsw > S(S_LSW) || u < e;
+      } else {
+        take = c_lsw > S(S_LSW) || u < ex(c_lsw - S(S_LSW));
+        lsw_new = lse(S(S_LSW), c_lsw);
+      }
+      double rho[NCH], psp[NCH], psm[NCH], rho_old[NCH];
+      if constexpr (FM) {   // branch-free: the sample point rewritten with a select (LDS image)
+        double o_q[NCH], o_g[NCH], nq[NCH], ng[NCH];
+        ld(vp(V_QS), o_q);
+        ld(vp(V_GS), o_g);
+        ld(vp(V_RHO), rho);
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+          nq[k] = take ? c_q[k] : o_q[k];
+          ng[k] = take ? c_g[k] : o_g[k];
+        }
+        st(vp(V_QS), nq);
+        st(vp(V_GS), ng);
+        S(S_VS) = take ? c_V : S(S_VS);
+        S(S_HS) = take ? c_H : S(S_HS);
+      } else {
+        if (take) {
+          st(vp(V_QS), c_q);
+          st(vp(V_GS), c_g);
+          S(S_VS) = c_V;
+          S(S_HS) = c_H;
+        }
+        ld(vp(V_RHO), rho);
+      }
+      S(S_LSW) = lsw_new;
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
-        nq[k] = take ? c_q[k] : o_q[k];
-        ng[k] = take ? c_g[k] : o_g[k];
+        rho_old[k] = rho[k];
+        rho[k] = rho[k] + c_rho[k];
       }
-      st(vp(V_QS), nq);
-      st(vp(V_GS), ng);
-      S(S_VS) = take ? c_V : S(S_VS);
-      S(S_HS) = take ? c_H : S(S_HS);
-    } else {
-      if (take) {
-        st(vp(V_QS), c_q);
-        st(vp(V_GS), c_g);
-        S(S_VS) = c_V;
-        S(S_HS) = c_H;
+      st(vp(V_RHO), rho);
+      if constexpr (FM) {   // the end this sub-tree extends gets its p_sharp; the other end's is read
+        double oth[NCH];
+        st(vp(fwd ? V_PSP : V_PSM), c_pse);
+        ld(vp(fwd ? V_PSM : V_PSP), oth);
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+          psp[k] = fwd ? c_pse[k] : oth[k];
+          psm[k] = fwd ? oth[k] : c_pse[k];
+        }
+      } else if (fwd) {
+        st(vp(V_PSP), c_pse);
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) psp[k] = c_pse[k];
+        ld(vp(V_PSM), psm);
+      } else {
+        st(vp(V_PSM), c_pse);
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) psm[k] = c_pse[k];
+        ld(vp(V_PSP), psp);
       }
-      ld(vp(V_RHO), rho);
-    }
-    S(S_LSW) = lsw_new;
+      bool junction_ok = true;
+      if (uext()) {
+        // the new sub-tree against the old trajectory across their junction (base_nuts::transition)
+        double e1[NCH], e2[NCH];
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      rho_old[k] = rho[k];
-      rho[k] = rho[k] + c_rho[k];
-    }
-    st(vp(V_RHO), rho);
-    if constexpr (FM) {   // the end this sub-tree extends gets its p_sharp; the other end's is read
-      double oth[NCH];
-      st(vp(fwd ? V_PSP : V_PSM), c_pse);
-      ld(vp(fwd ? V_PSM : V_PSP), oth);
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        psp[k] = fwd ? c_pse[k] : oth[k];
-        psm[k] = fwd ? oth[k] : c_pse[k];
+        for (int k = 0; k < NCH; ++k) {
+          e1[k] = fwd ? rho_old[k] + c_pb[k] : c_rho[k] + o_p[k];
+          e2[k] = fwd ? c_rho[k] + o_p[k] : rho_old[k] + c_pb[k];
+        }
+        const bool ok2 = fwd ? criterion(psm, c_psb, e1) : criterion(c_pse, o_ps, e1);
+        const bool ok3 = fwd ? criterion(o_ps, c_pse, e2) : criterion(c_psb, psp, e2);
+        junction_ok = ok2 && ok3;
       }
-    } else if (fwd) {
-      st(vp(V_PSP), c_pse);
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) psp[k] = c_pse[k];
-      ld(vp(V_PSM), psm);
-    } else {
-      st(vp(V_PSM), c_pse);
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) psm[k] = c_pse[k];
-      ld(vp(V_PSP), psp);
-    }
-    bool junction_ok = true;
-    if (uext()) {
-      // the new sub-tree against the old trajectory across their junction (base_nuts::transition)
-      double e1[NCH], e2[NCH];
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        e1[k] = fwd ? rho_old[k] + c_pb[k] : c_rho[k] + o_p[k];
-        e2[k] = fwd ? c_rho[k] + o_p[k] : rho_old[k] + c_pb[k];
+      stop = !junction_ok || !criterion(psm, psp, rho) || IV(I_DEPTH) >= A.max_depth;
+      if (!stop) {
+        begin_subtree();
+        return true;
       }
-      const bool ok2 = fwd ? criterion(psm, c_psb, e1) : criterion(c_pse, o_ps, e1);
-      const bool ok3 = fwd ? criterion(o_ps, c_pse, e2) : criterion(c_psb, psp, e2);
-      junction_ok = ok2 && ok3;
     }
-    if (!junction_ok) return end_transition(pause_at);
-    if (!criterion(psm, psp, rho) || IV(I_DEPTH) >= A.max_depth) return end_transition(pause_at);
-    begin_subtree();
-    return true;
+    return end_transition(pause_at);
   }
 
   // Consume the evaluation requested last step.  Returns true if a new request (at q) was issued.
