@@ -40,21 +40,16 @@ def instrument(s):
     body_end = s.index("  // Consume the evaluation requested last step.")
     leaf = s[body_start:body_end]
     leaf = leaf.replace("    finish_leapfrog(lp, glp);\n    ++nleap;", "    const unsigned long long tl0 = stamp();\n    finish_leapfrog(lp, glp);\n    ++nleap;", 1)
-    leaf = leaf.replace("    if (IV(I_DIV)) return end_transition(pause_at);\n    const int depth = IV(I_DEPTH);",
-                        "    stp[2] += stamp() - tl0;\n    if (IV(I_DIV)) return endt(pause_at);\n    const int depth = IV(I_DEPTH);", 1)
+    leaf = leaf.replace("    bool stop = IV(I_DIV) != 0;\n", "    stp[2] += stamp() - tl0;\n    bool stop = IV(I_DIV) != 0;\n", 1)
     leaf = leaf.replace("    int j = 0;\n", "    const unsigned long long tm0 = stamp();\n    int j = 0;\n", 1)
-    leaf = leaf.replace("      if (!ok1 || !junction_ok) return end_transition(pause_at);",
-                        "      if (!ok1 || !junction_ok) { stp[3] += stamp() - tm0; return endt(pause_at); }", 1)
-    leaf = leaf.replace("    if (j < depth) {\n", "    stp[3] += stamp() - tm0;\n    if (j < depth) {\n      const unsigned long long tp0 = stamp();\n", 1)
+    leaf = leaf.replace("    if (!stop && j < depth) {\n", "    stp[3] += stamp() - tm0;\n    if (!stop && j < depth) {\n      const unsigned long long tp0 = stamp();\n", 1)
     leaf = leaf.replace("      begin_leapfrog(IV(I_DIR) * S(S_EPS));\n      return true;\n    }",
                         "      begin_leapfrog(IV(I_DIR) * S(S_EPS));\n      stp[4] += stamp() - tp0;\n      return true;\n    }", 1)
-    leaf = leaf.replace("    // the top-level sub-tree of this depth is complete and valid\n",
-                        "    // the top-level sub-tree of this depth is complete and valid\n    const unsigned long long tt0 = stamp();\n", 1)
-    leaf = leaf.replace("    if (!junction_ok) return end_transition(pause_at);\n    if (!criterion(psm, psp, rho) || IV(I_DEPTH) >= A.max_depth) return end_transition(pause_at);\n    begin_subtree();\n    return true;",
-                        "    if (!junction_ok) { stp[5] += stamp() - tt0; return endt(pause_at); }\n"
-                        "    if (!criterion(psm, psp, rho) || IV(I_DEPTH) >= A.max_depth) { stp[5] += stamp() - tt0; return endt(pause_at); }\n"
-                        "    begin_subtree();\n    stp[5] += stamp() - tt0;\n    return true;", 1)
-    assert leaf.count("stamp()") == 11, leaf.count("stamp()")
+    leaf = leaf.replace("      // the top-level sub-tree of this depth is complete and valid\n",
+                        "      // the top-level sub-tree of this depth is complete and valid\n      const unsigned long long tt0 = stamp();\n", 1)
+    leaf = leaf.replace("      if (!stop) {\n        begin_subtree();\n        return true;\n      }\n    }\n    return end_transition(pause_at);",
+                        "      stp[5] += stamp() - tt0;\n      if (!stop) {\n        begin_subtree();\n        return true;\n      }\n    }\n    return endt(pause_at);", 1)
+    assert leaf.count("stamp()") == 8, leaf.count("stamp()")
     s = s[:body_start] + leaf + s[body_end:]
     # the fused loop
     sub("        const double lp = schools_lpgrad<NCH, SEG, true>(yc, isc, ch.q, glp, lane, ch.D, mtab);\n        ++steps;\n        req = ch.consume(lp, glp, pause_at);",
