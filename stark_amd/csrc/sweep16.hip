@@ -25,8 +25,8 @@
 //             logit_resid4 below; linear: z = (y - eta)/sigma;
 //   backward  G[16 cols][16 chains] += X_tile^T . d_eta: the D layout of the forward is the B
 //             layout of the backward (k-step s = rows 4s..4s+3 = register s), one MFMA per
-//             (16-column tile, k-step); a last tile of <= 4 columns runs on the VALU (16 FMAs
-//             instead of 4 mostly-padding MFMAs).
+//             (16-column tile, k-step); a last tile of <= 4 columns runs on the VALU (16 DPP
+//             FMAs instead of 4 mostly-padding MFMAs).
 // Chunk partials are summed in chunk order by k_sweep_reduce (sweep.hip): the gradient is
 // bitwise independent of how many shards share a launch or which GPU runs a shard.
 #include "sweep_common.h"
@@ -83,7 +83,6 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   char* const slot = reinterpret_cast<char*>(lds) + (size_t)w * SS;
   double* const tab = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (size_t)NW * SS);
-  double* const xst = tab + (LOGI ? EX_TAB : 0) + w * 64;      // the last tile's <= 4 columns x 16 rows
   if constexpr (LOGI) exp_table_init(tab);
   const double* qs = A.q + (size_t)shard * C * A.Dp;
   double bf[KF];                   // beta_{lr} at the column k-step s of lane group lh takes (forward)
@@ -166,7 +165,10 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
 #pragma unroll
         for (int t = 0; t < JTM; ++t) xa[s][t] = xs[(lh + 4 * s) * d + bcol(t)];
     }
-    if constexpr (g.VREM) xst[lane] = xs[(lane >> 2) * d + std::min(16 * JTM + (lane & 3), d - 1)];
+    // the VALU last tile's X: ONE value per lane, row lh + 4 (lr >> 2), column 16 JTM + (lr & 3) --
+    // the value of (row lh + 4i, column jj) is then lane 4i + jj of the lane's own DPP row
+    double xv = 0.0;
+    if constexpr (g.VREM) xv = xs[(lh + 4 * (lr >> 2)) * d + std::min(16 * JTM + (lr & 3), d - 1)];
     uint32_t ym[4];
     double yv[4];
 #pragma unroll
@@ -230,15 +232,20 @@ __global__ __launch_bounds__(256, 2) void k_sweep16(SweepArgs A) {
       for (int t = 0; t < JTM; ++t)
         gacc[t] = mfma_f64(PRE ? xa[s][t] : xs[(lh + 4 * s) * d + bcol(t)], de[s], gacc[t]);
     if constexpr (g.VREM) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const dbl2* p = reinterpret_cast<const dbl2*>(xst + (lh + 4 * i) * 4);
-        const dbl2 a0 = p[0], a1 = p[1];
-        gv[0] = fma(a0.x, de[i], gv[0]);
-        gv[1] = fma(a0.y, de[i], gv[1]);
-        gv[2] = fma(a1.x, de[i], gv[2]);
-        gv[3] = fma(a1.y, de[i], gv[3]);
-      }
+      // gv[jj] += X[lh + 4i][16 JTM + jj] * de[i] with the X value broadcast from lane 4i + jj of
+      // the row by v_fmac_f64_dpp row_newbcast (DPP64): no LDS copy of the last columns, 512 B
+      // instead of 8.5 KB of LDS traffic per sub-tile (A/B at d = 100: -0.8 / -1.1 % on two
+      // boxes, profiles/r05j_*, r05l_*).  s_nop 1: the two wait states a VALU write of the DPP
+      // source needs before the DPP read, should the register allocator copy xv
+#define S16_DPP_FMAC(I, J, G) "v_fmac_f64_dpp %" #G ", %4, %" #I " row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"
+      asm volatile("s_nop 1\n\t"
+                   S16_DPP_FMAC(5, 0, 0) S16_DPP_FMAC(5, 1, 1) S16_DPP_FMAC(5, 2, 2) S16_DPP_FMAC(5, 3, 3)
+                   S16_DPP_FMAC(6, 4, 0) S16_DPP_FMAC(6, 5, 1) S16_DPP_FMAC(6, 6, 2) S16_DPP_FMAC(6, 7, 3)
+                   S16_DPP_FMAC(7, 8, 0) S16_DPP_FMAC(7, 9, 1) S16_DPP_FMAC(7, 10, 2) S16_DPP_FMAC(7, 11, 3)
+                   S16_DPP_FMAC(8, 12, 0) S16_DPP_FMAC(8, 13, 1) S16_DPP_FMAC(8, 14, 2) S16_DPP_FMAC(8, 15, 3)
+                   : "+v"(gv[0]), "+v"(gv[1]), "+v"(gv[2]), "+v"(gv[3])
+                   : "v"(xv), "v"(de[0]), "v"(de[1]), "v"(de[2]), "v"(de[3]));
+#undef S16_DPP_FMAC
     }
     if constexpr (!PRE) {
       __builtin_amdgcn_s_waitcnt(0xC07F);              // lgkmcnt(0): the slot is free
@@ -314,7 +321,7 @@ using namespace stk;
 size_t stk_sweep16_lds_bytes(int family, int d) {
   const int KF = (d + 3) / 4;
   const S16Geom g = s16_geom(KF);
-  size_t main = (size_t)SM_W * sweepm_slot_bytes(d) + (family == STK_LOGREG ? EX_TAB * 8 : 0) + (size_t)SM_W * 64 * 8;
+  size_t main = (size_t)SM_W * sweepm_slot_bytes(d) + (family == STK_LOGREG ? EX_TAB * 8 : 0);
   const size_t red = ((size_t)SM_W * g.JT * 16 * 16 + (size_t)SM_W * 64 * 2 + (size_t)SM_W * 4 * 4 * 16) * 8;
   return std::max(main, red);
 }
