@@ -165,4 +165,189 @@ __global__ __launch_bounds__(512, 1) void k_gemm_fwd8(SweepArgs A) {
 template <int FAM, int NS>
 constexpr size_t gemm_fwd8_lds() { return (size_t)NS * (128 * 32 * 8 + 32 * 512) + EX_TAB * 8; }
 
+// Pass F with a PIPELINED epilogue: the tile's eta (accumulators + alpha) is parked in registers at
+// its last stage, and its residual / R stores / lp terms run one chain tile per stage during the
+// next tile's first stages (chain tile c2 at stage kc with c2 % NKC == kc), interleaved with their
+// MFMAs, instead of all 16 (row, chain) elements at the tile's end followed by vmcnt(0) -- the
+// unrolled 16-element epilogue is what holds the product kernel at 229 VGPRs (83 without it) and
+// what every wave of a block runs at once.  EPRE: the chain tile's residual before the stage's
+// MFMAs (its R stores then have the whole stage before the next vmcnt(0)); else after them.
+// Per chain tile the lp terms are added in the product's order: lp and the gradient are
+// bit-identical to k_gemm_fwd's.
+template <int FAM, bool EPRE>
+__global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd_p(SweepArgs A) {
+  constexpr int NW = G5_FW, NS = G5_FS, NCT = 16 / NW;
+  constexpr int KCF = G5_FKC, STG = g5_fstage_bytes(), XB = STG / 2;
+  constexpr int PPR = KCF / 2;
+  constexpr int NDMA = (XB / 1024) / NW;
+  static_assert(NDMA >= 1 && NS == 2, "pass F stage geometry");
+  auto swz = [](int row) { return PPR == 16 ? (row & 15) : ((row >> 1) & 7); };
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d, KP = g5_kp(d), NKC = KP / KCF;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int wr = w & 3, wc = w >> 2;
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * G5_TR, r1 = std::min<int64_t>(sh.n, t1 * G5_TR);
+  const int nrows = (int)(r1 - r0);
+  const int ntile = (int)(t1 - t0);
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const stg = reinterpret_cast<char*>(lds);
+  double* const sptab = reinterpret_cast<double*>(stg + NS * STG);
+  if constexpr (FAM == STK_LOGREG) exp_table_init(sptab);
+  const double* qb = A.q + (size_t)shard * G5_C * A.Dp;
+  double alpha[NCT], inv_s[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) {
+    const int ct = NCT * wc + c2;
+    alpha[c2] = qb[(size_t)(16 * ct + lr) * A.Dp];
+    inv_s[c2] = (FAM == STK_LINREG) ? exp(-qb[(size_t)(16 * ct + lr) * A.Dp + d + 1]) : 0.0;
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0xF70);
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
+  const __amdgpu_buffer_rsrc_t br = uniform_rsrc(A.qT + (size_t)shard * KP * G5_C, (int64_t)KP * G5_C * 8);
+  int xvo[NDMA];
+#pragma unroll
+  for (int i = 0; i < NDMA; ++i) {
+    const int sl = (w * NDMA + i) * 64 + lane, row = sl / PPR, pc = (sl % PPR) ^ swz(row);
+    xvo[i] = row * d * 8 + pc * 16;
+  }
+  auto issue = [&](int st) {
+    const int tile = st / NKC, kc = st % NKC;
+    char* b = stg + (st % NS) * STG;
+    const int xso = tile * G5_TR * d * 8 + kc * KCF * 8;
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * NDMA + i) * 1024), 16, xvo[i], xso, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(br, (lds_vptr)(b + XB + (w * NDMA + i) * 1024), 16, lane * 16,
+                                               kc * KCF * 512 + (w * NDMA + i) * 1024, 0, 0);
+  };
+  double lm[NCT], sp[NCT], ll[NCT], gaa[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) lm[c2] = sp[c2] = ll[c2] = gaa[c2] = 0.0;
+  char* const Rimg = reinterpret_cast<char*>(A.R + ((size_t)shard * A.Rrows + r0) * G5_C);
+  const int nst = ntile * NKC;
+  issue(0);
+  dbl4 acc[NCT];
+  double pend[NCT][4];                                  // eta of the parked tile
+  double yt[4] = {0.0, 0.0, 0.0, 0.0}, pyt[4] = {0.0, 0.0, 0.0, 0.0};
+  uint32_t yit[4] = {0u, 0u, 0u, 0u}, pyit[4] = {0u, 0u, 0u, 0u};
+  int ptile = -1;
+  auto epi = [&](auto c2c) {                            // the parked tile's chain tile c2
+    constexpr int c2 = decltype(c2c)::value;
+    const int ct = NCT * wc + c2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 16 * wr + lh + 4 * i;
+      const int64_t grow = (int64_t)ptile * G5_TR + row;
+      const bool valid = grow < nrows;
+      const double eta = pend[c2][i];
+      double dv;
+      if constexpr (FAM == STK_LOGREG) {
+        double lm2 = lm[c2], sp2 = sp[c2];
+        dv = -logit_resid4(eta, pyit[i], sptab, lm2, sp2);
+        lm[c2] = valid ? lm2 : lm[c2];
+        sp[c2] = valid ? sp2 : sp[c2];
+      } else {
+        const double z = (pyt[i] - eta) * inv_s[c2];
+        lm[c2] += valid ? z * z : 0.0;
+        dv = z * inv_s[c2];
+      }
+      dv = valid ? dv : 0.0;
+      gaa[c2] += dv;
+      *reinterpret_cast<double*>(Rimg + g5_chain_off((int)grow, 16 * ct + lr)) = dv;
+    }
+    if constexpr (FAM == STK_LOGREG) {
+      if ((ptile & 63) == 63) {
+        ll[c2] += log1p(sp[c2]);
+        sp[c2] = 0.0;
+      }
+    }
+  };
+  auto epi_stage = [&](int kc) {
+    if (ptile >= 0) {
+      if (0 % NKC == kc) epi(std::integral_constant<int, 0>{});
+      if (NCT > 1 && 1 % NKC == kc) epi(std::integral_constant<int, 1 % NCT>{});
+      if (NCT > 2 && 2 % NKC == kc) epi(std::integral_constant<int, 2 % NCT>{});
+      if (NCT > 3 && 3 % NKC == kc) epi(std::integral_constant<int, 3 % NCT>{});
+    }
+  };
+  for (int st = 0; st < nst; ++st) {
+    const int kc = st % NKC;
+    if (kc == 0) {
+#pragma unroll
+      for (int c2 = 0; c2 < NCT; ++c2) acc[c2] = dbl4{0.0, 0.0, 0.0, 0.0};
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70);                   // vmcnt(0): stage st landed, the last R stores retired
+    lds_barrier();
+    if (st + 1 < nst) issue(st + 1);
+    if (kc == 0) {
+      const int64_t tb = (int64_t)(st / NKC) * G5_TR + 16 * wr + lh;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t grow = tb + 4 * i;
+        if constexpr (FAM == STK_LOGREG) yit[i] = grow < nrows ? (uint32_t)sh.yi[r0 + grow] : 0u;
+        else yt[i] = grow < nrows ? sh.y[r0 + grow] : 0.0;
+      }
+    }
+    if constexpr (EPRE) epi_stage(kc);
+    const char* b = stg + (st % NS) * STG;
+    const int r = 16 * wr + lr;
+#pragma unroll
+    for (int step = 0; step < KCF / 4; ++step) {
+      const int kk = 4 * step + lh;
+      const double a = *reinterpret_cast<const double*>(b + r * (16 * PPR) + (((kk >> 1) ^ swz(r)) << 4) + ((kk & 1) << 3));
+#pragma unroll
+      for (int c2 = 0; c2 < NCT; ++c2)
+        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + XB + g5_chain_off(kk, 16 * (NCT * wc + c2) + lr)), acc[c2]);
+    }
+    if constexpr (!EPRE) epi_stage(kc);
+    if (kc == NKC - 1) {                                 // park this tile for the next tile's stages
+#pragma unroll
+      for (int c2 = 0; c2 < NCT; ++c2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pend[c2][i] = acc[c2][i] + alpha[c2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pyit[i] = yit[i];
+        pyt[i] = yt[i];
+      }
+      ptile = st / NKC;
+    }
+  }
+  if (ptile >= 0) {                                     // the chunk's last tile
+    epi(std::integral_constant<int, 0>{});
+    if constexpr (NCT > 1) epi(std::integral_constant<int, 1 % NCT>{});
+    if constexpr (NCT > 2) epi(std::integral_constant<int, 2 % NCT>{});
+    if constexpr (NCT > 3) epi(std::integral_constant<int, 3 % NCT>{});
+  }
+  double lpa[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] = (FAM == STK_LOGREG) ? 0.5 * lm[c2] - (ll[c2] + log1p(sp[c2])) : lm[c2];
+  __syncthreads();
+  double* red = lds;
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) {
+    red[((w * 64 + lane) * NCT + c2) * 2 + 0] = lpa[c2];
+    red[((w * 64 + lane) * NCT + c2) * 2 + 1] = gaa[c2];
+  }
+  __syncthreads();
+  if (tid < 2 * G5_C) {
+    const int c = tid >> 1, kind = tid & 1, ct = c >> 4, l = c & 15, cw = ct / NCT, c2 = ct % NCT;
+    double v = 0.0;
+    for (int ww = 0; ww < 4; ++ww)
+      for (int h = 0; h < 4; ++h) v += red[(((cw * 4 + ww) * 64 + h * 16 + l) * NCT + c2) * 2 + kind];
+    A.partial[(((size_t)shard * A.Gs + chunk) * G5_C + c) * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
+}
+
 }  // namespace stk
