@@ -122,8 +122,12 @@ int main(int argc, char** argv) {
     arms.push_back(Arm{"F8-s2", (const void*)k_gemm_fwd8<STK_LOGREG, 2>, 2, gemm_fwd8_lds<STK_LOGREG, 2>(), true, {}});
     arms.push_back(Arm{"F8-s3", (const void*)k_gemm_fwd8<STK_LOGREG, 3>, 2, gemm_fwd8_lds<STK_LOGREG, 3>(), true, {}});
   }
-  arms.push_back(Arm{"F-pipe-pre", (const void*)k_gemm_fwd_p<STK_LOGREG, true>, 0, lds, true, {}});
-  arms.push_back(Arm{"F-pipe-post", (const void*)k_gemm_fwd_p<STK_LOGREG, false>, 0, lds, true, {}});
+  if (getenv("GEMM_AB_PIPE")) {
+    arms.push_back(Arm{"F-pipe-pre", (const void*)k_gemm_fwd_p<STK_LOGREG, true>, 0, lds, true, {}});
+    arms.push_back(Arm{"F-pipe-post", (const void*)k_gemm_fwd_p<STK_LOGREG, false>, 0, lds, true, {}});
+  }
+  arms.push_back(Arm{"F-w128", (const void*)k_gemm_fwd_w<STK_LOGREG, 4>, 0, gemm_fwd_w_lds<STK_LOGREG, 4>(), true, {}});
+  arms.push_back(Arm{"F-w256", (const void*)k_gemm_fwd_w<STK_LOGREG, 8>, 2, gemm_fwd_w_lds<STK_LOGREG, 8>(), true, {}});
   if (getenv("GEMM_AB_TILES")) {
     arms.push_back(Arm{"F-r1k32s2", gemm_fwd_t_ptr<2, 32, 1>(), 0, gemm_fwd_t_lds<2, 32, 1>(), true, {}});
     arms.push_back(Arm{"F-r2k16s2", gemm_fwd_t_ptr<2, 16, 2>(), 0, gemm_fwd_t_lds<2, 16, 2>(), true, {}});

@@ -350,4 +350,207 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd_p(SweepArgs 
   }
 }
 
+// Pass F with 128-row tiles on the product's 4-wave block (two blocks per CU): each wave 32 rows
+// (two 16-row MFMA tiles) x all 64 chains, stages of 16 columns (X 16 KB + beta^T 8 KB) in a 3-deep
+// ring -- 80 KB per block with the table, two blocks fill the CU's 160 KB -- so one beta^T stage
+// feeds 128 rows (LDS-DMA volume 1.5 x the X bytes instead of 2 x) while one block's epilogue still
+// overlaps the other's MFMAs.  The 64 accumulators per wave leave no room for an all-at-once
+// epilogue (round 4's 128-row tiles spilled 70 VGPRs), so it is pipelined as in k_gemm_fwd_p: the
+// tile's eta parked, one (row tile, chain tile) part of 4 elements per stage of the next tile.
+// Waits: the LDS-DMA loads and the tile's y loads complete in issue order, so "at most the next
+// stage's DMA outstanding" proves the current stage landed whatever the R stores in between do;
+// the stores go out right after the barrier, a whole stage ahead of the wait that also counts them.
+// The DMA goes through a plain function: clang's host pass drops a kernel template's stub when the
+// builtin's operands depend on a template parameter (undefined symbol at link, no diagnostic).
+__device__ __forceinline__ void dma16_lds(__amdgpu_buffer_rsrc_t r, char* dst, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)dst, 16, voff, soff, 0, 0);
+}
+
+template <int FAM, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd_w(SweepArgs A) {
+  constexpr int NCT = 4, RT = 2, TR = 32 * NW, KCF = 16, NS = 3;
+  constexpr int XB = TR * KCF * 8, BB = KCF * 512, STG = XB + BB;
+  constexpr int PPR = KCF / 2;                          // 16-B pieces per X row in the stage (8)
+  constexpr int NDX = XB / 1024 / NW, NDB = BB / 1024 / NW, NPART = RT * NCT;
+  static_assert(NDX == 4 && NDB >= 1 && BB % (1024 * NW) == 0, "pass Fw stage geometry");
+  auto swz = [](int row) { return (row >> 1) & 7; };
+  const int shard = A.shard0 + blockIdx.x / A.G;
+  const int chunk = blockIdx.x % A.G;
+  if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
+  if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
+  const ShardDev sh = A.shards[shard];
+  const int d = sh.d, KP = (d + KCF - 1) / KCF * KCF, NKC = KP / KCF;
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;
+  const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
+  const int64_t r0 = t0 * G5_TR, r1 = std::min<int64_t>(sh.n, t1 * G5_TR);
+  const int nrows = (int)(r1 - r0);
+  const int rcap = (int)((t1 - t0) * G5_TR);
+  const int ntile = (rcap + TR - 1) / TR;
+
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  char* const stg = reinterpret_cast<char*>(lds);
+  double* const sptab = reinterpret_cast<double*>(stg + NS * STG);
+  if constexpr (FAM == STK_LOGREG) exp_table_init(sptab);
+  const double* qb = A.q + (size_t)shard * G5_C * A.Dp;
+  double alpha[NCT], inv_s[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) {
+    alpha[c2] = qb[(size_t)(16 * c2 + lr) * A.Dp];
+    inv_s[c2] = (FAM == STK_LINREG) ? exp(-qb[(size_t)(16 * c2 + lr) * A.Dp + d + 1]) : 0.0;
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0xF70);
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
+  // beta^T rows past the image's KP (a multiple of 32) read as 0 through the descriptor bound
+  const int KPI = g5_kp(d);
+  const __amdgpu_buffer_rsrc_t br = uniform_rsrc(A.qT + (size_t)shard * KPI * G5_C, (int64_t)KPI * G5_C * 8);
+  int xvo[NDX];
+#pragma unroll
+  for (int i = 0; i < NDX; ++i) {
+    const int sl = (w * NDX + i) * 64 + lane, row = sl / PPR, pc = (sl % PPR) ^ swz(row);
+    xvo[i] = row * d * 8 + pc * 16;
+  }
+  auto issue = [&](int st) {
+    const int tile = st / NKC, kc = st % NKC;
+    char* b = stg + (st % NS) * STG;
+    const int xso = tile * TR * d * 8 + kc * KCF * 8;
+#pragma unroll
+    for (int i = 0; i < NDX; ++i)
+      dma16_lds(xr, b + (w * NDX + i) * 1024, xvo[i], xso);
+#pragma unroll
+    for (int i = 0; i < NDB; ++i)
+      dma16_lds(br, b + XB + (w * NDB + i) * 1024, lane * 16, kc * KCF * 512 + (w * NDB + i) * 1024);
+  };
+  // lm = sum (t - |t|) - 2 sum log1p(sp) at the flushes (the flushed logs folded in: no ll registers)
+  double lm[NCT], sp[NCT], gaa[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) lm[c2] = sp[c2] = gaa[c2] = 0.0;
+  char* const Rimg = reinterpret_cast<char*>(A.R + ((size_t)shard * A.Rrows + r0) * G5_C);
+  const int nst = ntile * NKC;
+  for (int s0 = 0; s0 < NS - 1 && s0 < nst; ++s0) issue(s0);
+  dbl4 acc[RT][NCT];
+  double pend[RT][NCT][4];
+  uint32_t ybit = 0u, pybit = 0u;                       // logistic y of the tile's 8 rows per lane, one bit each
+  double yt[RT][4] = {}, pyt[RT][4] = {};
+  int ptile = -1;
+  auto epi = [&](const int p) {                         // part p = (row tile p / NCT, chain tile p % NCT);
+    const int rt = p / NCT, c2 = p % NCT;                // called from unrolled loops: p is a constant
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int grow = ptile * TR + 32 * w + 16 * rt + lh + 4 * i;
+      const bool valid = grow < nrows;
+      const double eta = pend[rt][c2][i];
+      double dv;
+      if constexpr (FAM == STK_LOGREG) {
+        double lm2 = lm[c2], sp2 = sp[c2];
+        dv = -logit_resid4(eta, (pybit >> (4 * rt + i)) & 1u, sptab, lm2, sp2);
+        lm[c2] = valid ? lm2 : lm[c2];
+        sp[c2] = valid ? sp2 : sp[c2];
+      } else {
+        const double z = (pyt[rt][i] - eta) * inv_s[c2];
+        lm[c2] += valid ? z * z : 0.0;
+        dv = z * inv_s[c2];
+      }
+      dv = valid ? dv : 0.0;
+      gaa[c2] += dv;
+      if (grow < rcap) *reinterpret_cast<double*>(Rimg + g5_chain_off(grow, 16 * c2 + lr)) = dv;
+    }
+    if (FAM == STK_LOGREG && rt == RT - 1) {
+      if ((ptile & 31) == 31) {                          // 32 tiles x 8 elements per chain tile and lane
+        lm[c2] -= 2.0 * log1p(sp[c2]);
+        sp[c2] = 0.0;
+      }
+    }
+  };
+  auto epi_stage = [&](int kc) {
+    if (ptile >= 0) {
+#pragma unroll
+      for (int p = 0; p < NPART; ++p)
+        if (p % NKC == kc) epi(p);
+    }
+  };
+  for (int st = 0; st < nst; ++st) {
+    const int kc = st % NKC;
+    if (kc == 0) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int c2 = 0; c2 < NCT; ++c2) acc[rt][c2] = dbl4{0.0, 0.0, 0.0, 0.0};
+    }
+    wait_vmcnt(std::min(NS - 2, nst - 1 - st) * (NDX + NDB));
+    lds_barrier();
+    epi_stage(kc);
+    if (kc == 0) {                                       // this tile's y (loads: in order with the DMA)
+      if constexpr (FAM == STK_LOGREG) ybit = 0u;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t grow = (int64_t)(st / NKC) * TR + 32 * w + 16 * rt + lh + 4 * i;
+          if constexpr (FAM == STK_LOGREG) ybit |= (grow < nrows ? (uint32_t)sh.yi[r0 + grow] & 1u : 0u) << (4 * rt + i);
+          else yt[rt][i] = grow < nrows ? sh.y[r0 + grow] : 0.0;
+        }
+    }
+    if (st + NS - 1 < nst) issue(st + NS - 1);
+    const char* b = stg + (st % NS) * STG;
+#pragma unroll
+    for (int step = 0; step < KCF / 4; ++step) {
+      const int kk = 4 * step + lh;
+      double a[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = 32 * w + 16 * rt + lr;
+        a[rt] = *reinterpret_cast<const double*>(b + r * (16 * PPR) + (((kk >> 1) ^ swz(r)) << 4) + ((kk & 1) << 3));
+      }
+#pragma unroll
+      for (int c2 = 0; c2 < NCT; ++c2) {
+        const double bb = *reinterpret_cast<const double*>(b + XB + g5_chain_off(kk, 16 * c2 + lr));
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt][c2] = mfma_f64(a[rt], bb, acc[rt][c2]);
+      }
+    }
+    if (kc == NKC - 1) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+        for (int c2 = 0; c2 < NCT; ++c2)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pend[rt][c2][i] = acc[rt][c2][i] + alpha[c2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pyt[rt][i] = yt[rt][i];
+      }
+      pybit = ybit;
+      ptile = st / NKC;
+    }
+  }
+  if (ptile >= 0) {
+#pragma unroll
+    for (int p = 0; p < NPART; ++p) epi(p);
+  }
+  double lpa[NCT];
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] = (FAM == STK_LOGREG) ? 0.5 * lm[c2] - log1p(sp[c2]) : lm[c2];
+  __builtin_amdgcn_s_waitcnt(0xF70);
+  __syncthreads();
+  double* red = lds;
+#pragma unroll
+  for (int c2 = 0; c2 < NCT; ++c2) {
+    red[((w * 64 + lane) * NCT + c2) * 2 + 0] = lpa[c2];
+    red[((w * 64 + lane) * NCT + c2) * 2 + 1] = gaa[c2];
+  }
+  __syncthreads();
+  if (tid < 2 * G5_C) {
+    const int c = tid >> 1, kind = tid & 1, c2 = c >> 4, l = c & 15;
+    double v = 0.0;
+    for (int ww = 0; ww < NW; ++ww)
+      for (int h = 0; h < 4; ++h) v += red[((ww * 64 + h * 16 + l) * NCT + c2) * 2 + kind];
+    A.partial[(((size_t)shard * A.Gs + chunk) * G5_C + c) * A.PW + (kind == 0 ? d + 1 : 0)] = v;
+  }
+}
+
+template <int FAM, int NW = 4>
+constexpr size_t gemm_fwd_w_lds() { return (size_t)3 * (32 * NW * 16 * 8 + 16 * 512) + EX_TAB * 8; }
+
 }  // namespace stk
