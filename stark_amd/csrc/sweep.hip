@@ -701,166 +701,198 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);                   // lgkmcnt(0): this wave's LDS accesses done
   __builtin_amdgcn_s_barrier();
 }
-constexpr int G5_FW = 4;      // pass F: waves per block (two blocks per CU; 8 waves, one block: slower)
-constexpr int G5_FS = 2;      // pass F: stages in the ring
-constexpr int G5_FKC = 32;    // pass F: columns per stage (32 KB stages; 16 columns x 4 stages: slower)
-__host__ __device__ constexpr int g5_fstage_bytes() { return 1024 * G5_FKC; }
+// Pass F geometry: tiles of G5_FTR = 32 G5_FW rows, G5_FW waves of 32 rows (2 MFMA row tiles) x
+// all 4 chain tiles each (8 accumulators, 64 VGPRs), 16-column stages in a 3-deep ring.
+constexpr int G5_FW = 4;      // pass F: waves per block (two blocks per CU share its 160 KB of LDS)
+constexpr int G5_FS = 3;      // pass F: stages in the ring
+constexpr int G5_FKC = 16;    // pass F: columns per stage
+constexpr int G5_FTR = 32 * G5_FW;   // pass F: rows per tile
+__host__ __device__ constexpr int g5_fstage_bytes() { return G5_FTR * G5_FKC * 8 + G5_FKC * 512; }   // [X][beta^T]
 
-// Pass F: one block per (shard, chunk); the chunk's 64-row tiles one after another.  NW waves
-// (4: two blocks per CU, a double buffer; 8: one block per CU, the 4-stage ring), each with
-// NCT = 16 / NW chain tiles.  With one block per CU every wave reaches the tile epilogue (the
-// residual, VALU) at once and the MFMAs idle meanwhile; two blocks overlap one's epilogue with
-// the other's GEMM, which measured faster for this pass.
-template <int FAM>
-__global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A) {
-  constexpr int NW = G5_FW, NS = G5_FS, NCT = 16 / NW;
-  constexpr int KCF = G5_FKC, STG = g5_fstage_bytes(), XB = STG / 2;   // stage: [X 64 x KCF][beta^T KCF x 64]
-  constexpr int PPR = KCF / 2;                          // 16-B pieces per X row in the stage
-  constexpr int NDMA = (XB / 1024) / NW;                // DMA instructions per wave per operand image
-  static_assert(NDMA >= 1, "pass F stage geometry");
-  // X piece swizzle: 256-B rows (PPR 16) XOR the piece with row & 15; 128-B rows (PPR 8) put
-  // rows of one parity on one half of the banks, so XOR with (row >> 1) & 7
-  auto swz = [](int row) { return PPR == 16 ? (row & 15) : ((row >> 1) & 7); };
+// The DMA goes through a plain function: clang's host pass drops a kernel template's stub when the
+// builtin's operands depend on a template parameter (undefined symbol at link, no diagnostic).
+__device__ __forceinline__ void dma16_lds(__amdgpu_buffer_rsrc_t r, char* dst, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)dst, 16, voff, soff, 0, 0);
+}
+
+// Pass F: one block per (shard, chunk); the chunk's 128-row tiles one after another.  A stage
+// is 16 columns of the tile's X (16 KB) and of beta^T (8 KB), so one beta^T stage feeds 128 rows
+// (LDS-DMA volume 1.5 x the X bytes; round 4's 64-row tiles: 2 x).  Two blocks per CU (72 KB of
+// LDS each with the exp table) overlap one block's epilogue with the other's MFMAs.  The 64
+// accumulators per lane leave no room for the whole tile's epilogue at once, so it is
+// pipelined: the finished tile's eta is parked, and one (row tile, chain tile) part of 4
+// elements is done per stage of the next tile (all 8 at the chunk's end if NKC < 8).
+// Waits: the LDS-DMA loads and the tile's y loads complete in issue order, so "at most the next
+// stage's DMA outstanding" proves the current stage landed whatever the R stores in between do
+// (a store still in flight only makes the count larger).  DESIGN.md section 3.
+template <int FAM, int NW = G5_FW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
+  constexpr int NCT = 4, RT = 2, TR = 32 * NW, KCF = G5_FKC, NS = G5_FS;
+  constexpr int XB = TR * KCF * 8, BB = KCF * 512, STG = XB + BB;
+  constexpr int PPR = KCF / 2;                          // 16-B pieces per X row in the stage (8)
+  constexpr int NDX = XB / 1024 / NW, NDB = BB / 1024 / NW, NPART = RT * NCT;
+  static_assert(NDX == 4 && NDB >= 1 && BB % (1024 * NW) == 0, "pass F stage geometry");
+  // X piece swizzle: 128-B rows put rows of one parity on one half of the banks, so XOR the
+  // piece with (row >> 1) & 7 (every A fragment read conflict free)
+  auto swz = [](int row) { return (row >> 1) & 7; };
   const int shard = A.shard0 + blockIdx.x / A.G;
   const int chunk = blockIdx.x % A.G;
   if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
   if (A.ran && chunk == 0 && threadIdx.x == 0) atomicAdd(&A.ran[A.step_id & 63], 1);
   const ShardDev sh = A.shards[shard];
-  const int d = sh.d, KP = g5_kp(d), NKC = KP / KCF;
+  const int d = sh.d, KP = (d + KCF - 1) / KCF * KCF, NKC = KP / KCF;
   const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
-  const int wr = w & 3, wc = w >> 2;
   const int lr = lane & 15, lh = lane >> 4;
+  // chunks are whole 64-row tiles of the shard (R's geometry, pass B's too); the last 128-row
+  // tile of a chunk may cover 64 rows past it: X reads there are 0 (descriptor bound), R stores skipped
   const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;
   const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
   const int64_t r0 = t0 * G5_TR, r1 = std::min<int64_t>(sh.n, t1 * G5_TR);
   const int nrows = (int)(r1 - r0);
-  const int ntile = (int)(t1 - t0);
+  const int rcap = (int)((t1 - t0) * G5_TR);
+  const int ntile = (rcap + TR - 1) / TR;
 
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  char* const stg = reinterpret_cast<char*>(lds);                 // NS stages of STG bytes
+  char* const stg = reinterpret_cast<char*>(lds);      // NS stages of STG bytes
   double* const sptab = reinterpret_cast<double*>(stg + NS * STG);
   if constexpr (FAM == STK_LOGREG) exp_table_init(sptab);
-
-  // per-lane chain constants: chain 16 ct + lr, ct = 2 wc + c2
+  // per-lane chain constants: chain 16 c2 + lr
   const double* qb = A.q + (size_t)shard * G5_C * A.Dp;
   double alpha[NCT], inv_s[NCT];
 #pragma unroll
   for (int c2 = 0; c2 < NCT; ++c2) {
-    const int ct = NCT * wc + c2;
-    alpha[c2] = qb[(size_t)(16 * ct + lr) * A.Dp];
-    inv_s[c2] = (FAM == STK_LINREG) ? exp(-qb[(size_t)(16 * ct + lr) * A.Dp + d + 1]) : 0.0;
+    alpha[c2] = qb[(size_t)(16 * c2 + lr) * A.Dp];
+    inv_s[c2] = (FAM == STK_LINREG) ? exp(-qb[(size_t)(16 * c2 + lr) * A.Dp + d + 1]) : 0.0;
   }
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(0xF70);
-
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
-  const __amdgpu_buffer_rsrc_t br = uniform_rsrc(A.qT + (size_t)shard * KP * G5_C, (int64_t)KP * G5_C * 8);
+  const int KPI = g5_kp(d);                             // beta^T image rows (>= KP, zero past d)
+  const __amdgpu_buffer_rsrc_t br = uniform_rsrc(A.qT + (size_t)shard * KPI * G5_C, (int64_t)KPI * G5_C * 8);
   // X stage: slot s (16 B) = row s / PPR, piece (s % PPR) ^ swz(row) of the stage's KCF columns
-  int xvo[NDMA];
+  int xvo[NDX];
 #pragma unroll
-  for (int i = 0; i < NDMA; ++i) {
-    const int sl = (w * NDMA + i) * 64 + lane, row = sl / PPR, pc = (sl % PPR) ^ swz(row);
+  for (int i = 0; i < NDX; ++i) {
+    const int sl = (w * NDX + i) * 64 + lane, row = sl / PPR, pc = (sl % PPR) ^ swz(row);
     xvo[i] = row * d * 8 + pc * 16;
   }
-  auto issue = [&](int st) {          // global stage index st = tile * NKC + kc
+  auto issue = [&](int st) {                            // global stage index st = tile * NKC + kc
     const int tile = st / NKC, kc = st % NKC;
     char* b = stg + (st % NS) * STG;
-    const int xso = tile * G5_TR * d * 8 + kc * KCF * 8;
+    const int xso = tile * TR * d * 8 + kc * KCF * 8;
 #pragma unroll
-    for (int i = 0; i < NDMA; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * NDMA + i) * 1024), 16, xvo[i], xso, 0, 0);
+    for (int i = 0; i < NDX; ++i) dma16_lds(xr, b + (w * NDX + i) * 1024, xvo[i], xso);
 #pragma unroll
-    for (int i = 0; i < NDMA; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(br, (lds_vptr)(b + XB + (w * NDMA + i) * 1024), 16, lane * 16,
-                                               kc * KCF * 512 + (w * NDMA + i) * 1024, 0, 0);
+    for (int i = 0; i < NDB; ++i) dma16_lds(br, b + XB + (w * NDB + i) * 1024, lane * 16, kc * KCF * 512 + (w * NDB + i) * 1024);
   };
-
-  // per chain tile: logistic lm = sum(t - |t|), sp = prod(1 + e) - 1, ll = the flushed log1p(sp)
+  // per chain tile: logistic lm = sum(t - |t|) - 2 sum(flushed log1p(sp)), sp = prod(1 + e) - 1
   // (residual v4, sweep_common.h); linear: lm = sum z^2
-  double lm[NCT], sp[NCT], ll[NCT], gaa[NCT];
+  double lm[NCT], sp[NCT], gaa[NCT];
 #pragma unroll
-  for (int c2 = 0; c2 < NCT; ++c2) lm[c2] = sp[c2] = ll[c2] = gaa[c2] = 0.0;
+  for (int c2 = 0; c2 < NCT; ++c2) lm[c2] = sp[c2] = gaa[c2] = 0.0;
   char* const Rimg = reinterpret_cast<char*>(A.R + ((size_t)shard * A.Rrows + r0) * G5_C);
   const int nst = ntile * NKC;
   for (int s0 = 0; s0 < NS - 1 && s0 < nst; ++s0) issue(s0);
-  dbl4 acc[NCT];
-  double yt[4] = {0.0, 0.0, 0.0, 0.0};                  // y of this lane's 4 rows of the current tile
-  uint32_t yit[4] = {0u, 0u, 0u, 0u};
+  dbl4 acc[RT][NCT];
+  double pend[RT][NCT][4];                              // the parked tile's eta
+  uint32_t ybit = 0u, pybit = 0u;                       // logistic y of this lane's 8 rows of the tile, one bit each
+  double yt[RT][4] = {}, pyt[RT][4] = {};               // linear y
+  int ptile = -1;
+  auto epi = [&](const int p) {                         // part p = (row tile p / NCT, chain tile p % NCT);
+    const int rt = p / NCT, c2 = p % NCT;                // called from unrolled loops: p is a constant
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int grow = ptile * TR + 32 * w + 16 * rt + lh + 4 * i;   // row of the chunk
+      const bool valid = grow < nrows;
+      const double eta = pend[rt][c2][i];
+      double dv;
+      if constexpr (FAM == STK_LOGREG) {
+        double lm2 = lm[c2], sp2 = sp[c2];
+        dv = -logit_resid4(eta, (pybit >> (4 * rt + i)) & 1u, sptab, lm2, sp2);
+        lm[c2] = valid ? lm2 : lm[c2];
+        sp[c2] = valid ? sp2 : sp[c2];
+      } else {
+        const double z = (pyt[rt][i] - eta) * inv_s[c2];
+        lm[c2] += valid ? z * z : 0.0;
+        dv = z * inv_s[c2];
+      }
+      dv = valid ? dv : 0.0;
+      gaa[c2] += dv;
+      if (grow < rcap) *reinterpret_cast<double*>(Rimg + g5_chain_off(grow, 16 * c2 + lr)) = dv;
+    }
+    if (FAM == STK_LOGREG && rt == RT - 1 && (ptile & 31) == 31) {   // 32 tiles x 8 elements per lane
+      lm[c2] -= 2.0 * log1p(sp[c2]);
+      sp[c2] = 0.0;
+    }
+  };
   for (int st = 0; st < nst; ++st) {
     const int kc = st % NKC;
     if (kc == 0) {
 #pragma unroll
-      for (int c2 = 0; c2 < NCT; ++c2) acc[c2] = dbl4{0.0, 0.0, 0.0, 0.0};
-    }
-    wait_vmcnt(std::min(NS - 2, nst - 1 - st) * 2 * NDMA);   // own DMAs of stage st retired (and the y loads)
-    lds_barrier();                                       // stage st landed for every wave; slot of st-1 free
-    if (st + NS - 1 < nst) issue(st + NS - 1);
-    if (kc == 0) {                                       // the tile's y, needed by its epilogue: one latency per tile
-      const int64_t tb = (int64_t)(st / NKC) * G5_TR + 16 * wr + lh;
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t grow = tb + 4 * i;
-        if constexpr (FAM == STK_LOGREG) yit[i] = grow < nrows ? (uint32_t)sh.yi[r0 + grow] : 0u;
-        else yt[i] = grow < nrows ? sh.y[r0 + grow] : 0.0;
-      }
+        for (int c2 = 0; c2 < NCT; ++c2) acc[rt][c2] = dbl4{0.0, 0.0, 0.0, 0.0};
     }
+    wait_vmcnt(std::min(NS - 2, nst - 1 - st) * (NDX + NDB));   // own DMAs of stage st retired
+    lds_barrier();                                       // stage st landed for every wave; slot of st-1 free
+    if (ptile >= 0) {                                    // the parked tile's parts due at this stage
+#pragma unroll
+      for (int p = 0; p < NPART; ++p)
+        if (p % NKC == kc) epi(p);
+    }
+    if (kc == 0) {                                       // this tile's y (loads: in order with the DMA)
+      if constexpr (FAM == STK_LOGREG) ybit = 0u;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t grow = (int64_t)(st / NKC) * TR + 32 * w + 16 * rt + lh + 4 * i;
+          if constexpr (FAM == STK_LOGREG) ybit |= (grow < nrows ? (uint32_t)sh.yi[r0 + grow] & 1u : 0u) << (4 * rt + i);
+          else yt[rt][i] = grow < nrows ? sh.y[r0 + grow] : 0.0;
+        }
+    }
+    if (st + NS - 1 < nst) issue(st + NS - 1);
     const char* b = stg + (st % NS) * STG;
-    const int r = 16 * wr + lr;
 #pragma unroll
     for (int step = 0; step < KCF / 4; ++step) {
       const int kk = 4 * step + lh;
-      const double a = *reinterpret_cast<const double*>(b + r * (16 * PPR) + (((kk >> 1) ^ swz(r)) << 4) + ((kk & 1) << 3));
+      double a[RT];
 #pragma unroll
-      for (int c2 = 0; c2 < NCT; ++c2)
-        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + XB + g5_chain_off(kk, 16 * (NCT * wc + c2) + lr)), acc[c2]);
-    }
-    if (kc == NKC - 1) {                                 // ---- tile epilogue: residual, R, lp
-      // straight from the accumulators, every (chain tile, row) unrolled: compile-time indices
-      // into alpha / lm / sp, and residual v4 (one exp per element, the logs as a running
-      // product per chain tile, flushed every 64 tiles = 256 elements)
-      const int tile = st / NKC;
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = 32 * w + 16 * rt + lr;
+        a[rt] = *reinterpret_cast<const double*>(b + r * (16 * PPR) + (((kk >> 1) ^ swz(r)) << 4) + ((kk & 1) << 3));
+      }
 #pragma unroll
       for (int c2 = 0; c2 < NCT; ++c2) {
-        const int ct = NCT * wc + c2;
+        const double bb = *reinterpret_cast<const double*>(b + XB + g5_chain_off(kk, 16 * c2 + lr));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 16 * wr + lh + 4 * i;              // row of the tile
-          const int64_t grow = (int64_t)tile * G5_TR + row;  // row of the chunk
-          const bool valid = grow < nrows;
-          const double eta = acc[c2][i] + alpha[c2];
-          double dv;
-          if constexpr (FAM == STK_LOGREG) {
-            double lm2 = lm[c2], sp2 = sp[c2];
-            dv = -logit_resid4(eta, yit[i], sptab, lm2, sp2);
-            lm[c2] = valid ? lm2 : lm[c2];
-            sp[c2] = valid ? sp2 : sp[c2];
-          } else {
-            const double z = (yt[i] - eta) * inv_s[c2];
-            lm[c2] += valid ? z * z : 0.0;
-            dv = z * inv_s[c2];
-          }
-          dv = valid ? dv : 0.0;
-          gaa[c2] += dv;
-          *reinterpret_cast<double*>(Rimg + g5_chain_off((int)grow, 16 * ct + lr)) = dv;
-        }
+        for (int rt = 0; rt < RT; ++rt) acc[rt][c2] = mfma_f64(a[rt], bb, acc[rt][c2]);
       }
-      if constexpr (FAM == STK_LOGREG) {
-        if ((tile & 63) == 63) {
-#pragma unroll
-          for (int c2 = 0; c2 < NCT; ++c2) {
-            ll[c2] += log1p(sp[c2]);
-            sp[c2] = 0.0;
-          }
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0xF70);                  // vmcnt(0): R stores retired before the next counted DMA wait
     }
+    if (kc == NKC - 1) {                                 // park the tile: its epilogue runs during the next
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+        for (int c2 = 0; c2 < NCT; ++c2)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pend[rt][c2][i] = acc[rt][c2][i] + alpha[c2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pyt[rt][i] = yt[rt][i];
+      }
+      pybit = ybit;
+      ptile = st / NKC;
+    }
+  }
+  if (ptile >= 0) {                                      // the last tile, and any parts NKC < 8 stages left over
+#pragma unroll
+    for (int p = 0; p < NPART; ++p) epi(p);
   }
   double lpa[NCT];
 #pragma unroll
-  for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] = (FAM == STK_LOGREG) ? 0.5 * lm[c2] - (ll[c2] + log1p(sp[c2])) : lm[c2];
+  for (int c2 = 0; c2 < NCT; ++c2) lpa[c2] = (FAM == STK_LOGREG) ? 0.5 * lm[c2] - log1p(sp[c2]) : lm[c2];
 
-  // ---- lp and sum(d eta) per chain: lanes lr of the 4 row groups h of the 4 waves wr, fixed order
+  // ---- lp and sum(d eta) per chain: lanes lr of the 4 row groups h of the NW waves, fixed order
+  __builtin_amdgcn_s_waitcnt(0xF70);
   __syncthreads();
   double* red = lds;                                     // [NW waves][64 lanes][NCT][2]
 #pragma unroll
@@ -870,10 +902,10 @@ __global__ __launch_bounds__(64 * G5_FW, 8 / G5_FW) void k_gemm_fwd(SweepArgs A)
   }
   __syncthreads();
   if (tid < 2 * G5_C) {
-    const int c = tid >> 1, kind = tid & 1, ct = c >> 4, l = c & 15, cw = ct / NCT, c2 = ct % NCT;
+    const int c = tid >> 1, kind = tid & 1, c2 = c >> 4, l = c & 15;
     double v = 0.0;
-    for (int ww = 0; ww < 4; ++ww)
-      for (int h = 0; h < 4; ++h) v += red[(((cw * 4 + ww) * 64 + h * 16 + l) * NCT + c2) * 2 + kind];
+    for (int ww = 0; ww < NW; ++ww)
+      for (int h = 0; h < 4; ++h) v += red[((ww * 64 + h * 16 + l) * NCT + c2) * 2 + kind];
     A.partial[(((size_t)shard * A.Gs + chunk) * G5_C + c) * A.PW + (kind == 0 ? d + 1 : 0)] = v;
   }
 }
@@ -1060,7 +1092,7 @@ static int sweep3_nb(int d, int C) {
 }
 
 static int sweep_variant(int64_t n, int d, int C) {
-  if (C == G5_C) return (((n + 511) / 512 + G5_TR) * d * 8 < ((int64_t)1 << 31)) ? 5 : 0;   // chunk bytes fit a buffer descriptor
+  if (C == G5_C) return (((n + 511) / 512 + G5_TR + G5_FTR) * d * 8 < ((int64_t)1 << 31)) ? 5 : 0;   // chunk bytes (+ pass F's last tile) fit a buffer descriptor
   if (C == SM_C) return (stk_sweep16_supported(d) && (n * d * 8) / 512 < ((int64_t)1 << 30)) ? 4 : 0;
   const int f = sweep_forced();
   const bool v3ok = d % 2 == 0 && d / 2 <= S3_KMAX && (C == 1 || C == 2 || C == 4) && sweep3_nb(d, C) >= 3 &&
@@ -1082,7 +1114,7 @@ void stk_sweep_geometry(int64_t n, int d, int* T, int* LD, int* G, size_t* lds_b
     *T = G5_TR;
     *LD = 0;
     *G = (int)g;
-    *lds_bytes = G5_FS * g5_fstage_bytes() + EX_TAB * sizeof(double);
+    *lds_bytes = G5_FS * g5_fstage_bytes() + EX_TAB * sizeof(double);   // pass F's (pass B sizes its own)
     return;
   }
   if (var == 4) {                       // k_sweep16 (sweep16.hip)

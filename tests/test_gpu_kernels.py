@@ -50,7 +50,10 @@ def test_schools_lpgrad(ctx, orc):
                                    # v5 two-pass fp64 MFMA GEMMs (64 chains; 70 = two batches)
                                    (1, 1, 64), (7, 3, 64), (4097, 50, 64), (333, 129, 64), (257, 300, 64),
                                    (1000, 1000, 64), (130, 1001, 70), (5000, 100, 64),
-                                   # pass F chunks of > 64 tiles of 64 rows (512 chunks per shard: n > 2.1e6),
+                                   # pass F's stage count per 128-row tile NKC = ceil(d / 16) at 1 and 2 (the
+                                   # parked tile's 8 epilogue parts mostly left for the next tile's end)
+                                   (300, 16, 64), (300, 17, 64),
+                                   # pass F chunks of > 32 tiles of 128 rows (512 chunks per shard: n > 2.1e6),
                                    # so its residual-v4 running product is flushed inside the loop too
                                    (2200000, 5, 64)])
 @pytest.mark.parametrize("family", ["logistic", "linear"])
