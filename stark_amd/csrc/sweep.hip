@@ -656,19 +656,18 @@ __global__ __launch_bounds__(512) void k_sweep3(SweepArgs A, int NBrt) {
 // workgroup's registers, so the sweep is split at the residual:
 //   pass F  eta = X . [beta_1 .. beta_64] (M = rows, N = chains, K = d), + alpha, residual
 //           on the fly: d eta -> R (HBM, 512 B per row), lp and sum(d eta) per chain;
-//   pass B  G = X^T . R (M = d, N = chains, K = rows) per (row chunk, 64-column block).
+//   pass B  G = X^T . R (M = d, N = chains, K = rows) per (row chunk, column block).
 // X crosses HBM twice per leapfrog (8d B per row each pass) plus R (1 KB per row), against
 // 4*d*64 flop per row: 15 flop/B at d = 1000, above the fp64 balance point, so both passes
-// are fp64-MFMA bound.  Both are the same LDS-staged GEMM skeleton:
-// 4 waves, double-buffered 16 KB + 16 KB stages moved by `buffer_load_dwordx4 ... lds`, a
-// k-step = one A fragment read + four B fragment reads (chain tiles) + four independent
-// v_mfma_f64_16x16x4_f64.  LDS images are XOR-swizzled in 16-B pieces so every fragment
-// read is bank-conflict free: X in pass F by per-lane DMA source offsets, beta^T and R by
-// their writers (k_qt_swizzle, pass F's epilogue).
+// are fp64-MFMA bound.  Both are LDS-staged GEMMs of 4 waves, two blocks
+// per CU, over rings of stages moved by `buffer_load_dwordx4 ... lds`; a wave holds 2 (pass F)
+// or 4 (pass B) 16-row tiles x all four 16-chain tiles, so a k-step is 2 or 4 A fragment reads
+// + four B fragment reads + 8 or 16 independent v_mfma_f64_16x16x4_f64.  LDS images are
+// XOR-swizzled in 16-B pieces so every fragment read is bank-conflict free: X by per-lane DMA
+// source offsets, beta^T and R by their writers (k_qt_swizzle, pass F's epilogue).
 constexpr int G5_C = 64;      // chains (4 MFMA N tiles)
-constexpr int G5_KC = 32;     // pass F: columns per stage
-constexpr int G5_TR = 64;     // pass F: rows per tile (16 per wave)
-constexpr int G5_RB = 32;     // pass B: rows per stage
+constexpr int G5_KC = 32;     // beta^T image rows: d rounded up to this
+constexpr int G5_TR = 64;     // chunk granularity in rows (R's rows: n rounded up to this)
 
 __host__ __device__ inline int g5_kp(int d) { return (d + G5_KC - 1) / G5_KC * G5_KC; }
 // byte offset of element (row r, chain c) in a 512-B-row chain image (beta^T rows k, R rows r)
@@ -687,13 +686,6 @@ __global__ __launch_bounds__(256) void k_qt_swizzle(SweepArgs A, int d) {
   *reinterpret_cast<double*>(img + g5_chain_off(k, c)) = v;
 }
 
-// Both passes: one block of G5_NW = 8 waves per CU (two per SIMD); wave w takes row / column
-// group w & 3 (16 rows or columns) and chain half w >> 2 (two 16-chain MFMA tiles), so every
-// output's K terms are summed in the same order as with one wave per group.  The stages run
-// through a ring of 4 LDS slots (128 KB): three stages are in flight while one is
-// consumed, and one barrier per stage both publishes the landed stage and frees the slot read
-// in the previous one (the refill of that slot is issued right after it).
-constexpr int G5_NW = 8;
 // A barrier that leaves LDS-DMAs in flight: __syncthreads() makes hipcc drain vmcnt(0) first
 // (an LDS-DMA is a pending LDS write on the VM counter), which would empty the stage ring at
 // every stage; the counted wait before it is what orders the DMA'd data.
@@ -911,18 +903,24 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
 }
 
 // Pass B: one block per (shard, chunk, JB-column block); G[j][c] += X[r][j] R[r][c] over the
-// chunk's rows, straight into the chunk's partial row (columns 1 .. d).  8 waves: wave w takes
-// column group w % WC (16 columns) and chain group w / WC (NCT 16-chain MFMA tiles); JB = 128
-// (default): 8 column groups x all 64 chains (4 MFMAs per A read), 48 KB stages in a 3-deep ring;
-// JB = 64: 4 column groups x 2 chain halves, 32 KB stages in a 4-deep ring (4 % slower).
-constexpr int G5_BJB = 128;   // pass B: columns per block (64: 4 % slower)
+// chunk's rows, straight into the chunk's partial row (columns 1 .. d).  4 waves, two blocks per
+// CU: wave w takes CTW = JB / 64 column tiles (16 columns each) x all 4 chain tiles (CTW A reads
+// + 4 B reads per 4 CTW MFMAs, 16 CTW accumulators), stages of 8 rows in a 3-deep ring.
+// JB = 256 (d > 128) re-reads each chunk's R from L2 once per column block: 4 x at d = 1000
+// (round 4's 128-column blocks: 8 x).  Every output sums its chunk's rows in row order.
+constexpr int G5_BRB = 8;     // pass B: rows per stage
+constexpr int G5_BW = 4;      // pass B: waves per block
 constexpr int G5_BNS = 3;     // pass B: stages in the ring
-__host__ __device__ constexpr int g5_bstage_bytes() { return 32 * G5_BJB * 8 + 16384; }
-__global__ __launch_bounds__(64 * G5_NW, 1) void k_gemm_bwd(SweepArgs A, int njb) {
-  constexpr int JB = G5_BJB, NSB = G5_BNS, WC = JB / 16, NCT = 4 * WC / G5_NW;
-  constexpr int XB = G5_RB * JB * 8, STG = g5_bstage_bytes(), PPR = JB / 2;
-  constexpr int NDX = XB / 1024 / G5_NW, NDR = 16384 / 1024 / G5_NW;   // DMA instructions per wave
-  static_assert(NDX >= 1 && NDR >= 1 && NCT >= 1 && STG == XB + 16384, "pass B stage geometry");
+__host__ __device__ constexpr int g5_bstage_bytes(int jb) { return G5_BRB * jb * 8 + G5_BRB * 512; }
+__host__ __device__ inline int g5_bjb(int d) { return d <= 64 ? 64 : d <= 128 ? 128 : 256; }
+template <int JB>
+__global__ __launch_bounds__(64 * G5_BW, 2) void k_gemm_bwd(SweepArgs A, int njb) {
+  constexpr int NW = G5_BW, RB = G5_BRB, NS = G5_BNS;
+  constexpr int CTW = JB / 16 / NW, NCT = 4, PPR = JB / 2;
+  constexpr int XB = RB * JB * 8, RBB = RB * 512, STG = XB + RBB;
+  constexpr int NDX = XB / 1024 / NW, NDR = RBB / 1024 / NW;   // DMA instructions per wave
+  static_assert(CTW >= 1 && NDX >= 1 && NDR >= 1 && XB % (1024 * NW) == 0 && RBB % (1024 * NW) == 0 &&
+                STG == g5_bstage_bytes(JB), "pass B stage geometry");
   // XCD-aware order: blocks are dealt to the 8 XCDs round-robin (blockIdx % 8), so the njb
   // column blocks of a chunk get blockIdx values of one residue -- one XCD, whose L2 then
   // serves the chunk's R rows to all of them (else each XCD re-reads R from HBM)
@@ -942,17 +940,16 @@ __global__ __launch_bounds__(64 * G5_NW, 1) void k_gemm_bwd(SweepArgs A, int njb
   const ShardDev sh = A.shards[shard];
   const int d = sh.d;
   const int tid = threadIdx.x, lane = tid & 63, w = uniform_int(tid >> 6);
-  const int cw = w % WC, cg = w / WC;
   const int lr = lane & 15, lh = lane >> 4;
   const int64_t nt = (sh.n + G5_TR - 1) / G5_TR;
   const int64_t t0 = nt * chunk / A.G, t1 = nt * (chunk + 1) / A.G;
   const int64_t r0 = t0 * G5_TR, r1 = std::min<int64_t>(sh.n, t1 * G5_TR);
   const int nrows = (int)(r1 - r0);
-  const int nst = (nrows + G5_RB - 1) / G5_RB;
+  const int nst = (nrows + RB - 1) / RB;
   const int j0 = jb * JB;
 
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  char* const stg = reinterpret_cast<char*>(lds);      // NSB stages: [X^T block XB][R block 16 KB]
+  char* const stg = reinterpret_cast<char*>(lds);      // NS stages: [X block XB][R block RBB]
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(sh.x + r0 * d, (int64_t)nrows * d * 8);
   const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(A.R + ((size_t)shard * A.Rrows + r0) * G5_C, (int64_t)nrows * G5_C * 8);
   // X stage: slot s = row s / PPR, piece (s % PPR) ^ ((row & 1) << 3) of the block's JB columns
@@ -964,44 +961,51 @@ __global__ __launch_bounds__(64 * G5_NW, 1) void k_gemm_bwd(SweepArgs A, int njb
     xvo[i] = row * d * 8 + (j0 + 2 * pc) * 8;
   }
   auto issue = [&](int st) {
-    char* b = stg + (st % NSB) * STG;
-    const int xso = st * G5_RB * d * 8;
+    char* b = stg + (st % NS) * STG;
+    const int xso = st * RB * d * 8;
 #pragma unroll
-    for (int i = 0; i < NDX; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_vptr)(b + (w * NDX + i) * 1024), 16, xvo[i], xso, 0, 0);
+    for (int i = 0; i < NDX; ++i) dma16_lds(xr, b + (w * NDX + i) * 1024, xvo[i], xso);
 #pragma unroll
-    for (int i = 0; i < NDR; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (lds_vptr)(b + XB + (w * NDR + i) * 1024), 16, lane * 16,
-                                               st * G5_RB * 512 + (w * NDR + i) * 1024, 0, 0);
+    for (int i = 0; i < NDR; ++i) dma16_lds(rr, b + XB + (w * NDR + i) * 1024, lane * 16, st * RB * 512 + (w * NDR + i) * 1024);
   };
-  dbl4 acc[NCT];
+  dbl4 acc[CTW][NCT];
 #pragma unroll
-  for (int c2 = 0; c2 < NCT; ++c2) acc[c2] = dbl4{0.0, 0.0, 0.0, 0.0};
-  for (int s0 = 0; s0 < NSB - 1 && s0 < nst; ++s0) issue(s0);
-  const int jl = 16 * cw + lr;                         // A row (column of X) of this lane
+  for (int ct = 0; ct < CTW; ++ct)
+#pragma unroll
+    for (int c2 = 0; c2 < NCT; ++c2) acc[ct][c2] = dbl4{0.0, 0.0, 0.0, 0.0};
+  for (int s0 = 0; s0 < NS - 1 && s0 < nst; ++s0) issue(s0);
   for (int st = 0; st < nst; ++st) {
-    wait_vmcnt(std::min(NSB - 2, nst - 1 - st) * (NDX + NDR));
+    wait_vmcnt(std::min(NS - 2, nst - 1 - st) * (NDX + NDR));
     lds_barrier();
-    if (st + NSB - 1 < nst) issue(st + NSB - 1);
-    const char* b = stg + (st % NSB) * STG;
+    if (st + NS - 1 < nst) issue(st + NS - 1);
+    const char* b = stg + (st % NS) * STG;
 #pragma unroll
-    for (int step = 0; step < G5_RB / 4; ++step) {
+    for (int step = 0; step < RB / 4; ++step) {
       const int r = 4 * step + lh;
-      const double a = *reinterpret_cast<const double*>(b + r * (16 * PPR) + ((((jl >> 1) ^ ((r & 1) << 3))) << 4) + ((jl & 1) << 3));
+      double a[CTW];
 #pragma unroll
-      for (int c2 = 0; c2 < NCT; ++c2)
-        acc[c2] = mfma_f64(a, *reinterpret_cast<const double*>(b + XB + g5_chain_off(r, 16 * (NCT * cg + c2) + lr)), acc[c2]);
+      for (int ct = 0; ct < CTW; ++ct) {
+        const int jl = 16 * (w * CTW + ct) + lr;       // A row (column of X) of this lane
+        a[ct] = *reinterpret_cast<const double*>(b + r * (16 * PPR) + ((((jl >> 1) ^ ((r & 1) << 3))) << 4) + ((jl & 1) << 3));
+      }
+#pragma unroll
+      for (int c2 = 0; c2 < NCT; ++c2) {
+        const double bb = *reinterpret_cast<const double*>(b + XB + g5_chain_off(r, 16 * c2 + lr));
+#pragma unroll
+        for (int ct = 0; ct < CTW; ++ct) acc[ct][c2] = mfma_f64(a[ct], bb, acc[ct][c2]);
+      }
     }
   }
   double* out = A.partial + ((size_t)shard * A.Gs + chunk) * G5_C * A.PW;
 #pragma unroll
-  for (int c2 = 0; c2 < NCT; ++c2) {
+  for (int ct = 0; ct < CTW; ++ct)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = j0 + 16 * cw + lh + 4 * i;
-      if (j < d) out[(size_t)(16 * (NCT * cg + c2) + lr) * A.PW + 1 + j] = acc[c2][i];
-    }
-  }
+    for (int c2 = 0; c2 < NCT; ++c2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = j0 + 16 * (w * CTW + ct) + lh + 4 * i;
+        if (j < d) out[(size_t)(16 * c2 + lr) * A.PW + 1 + j] = acc[ct][c2][i];
+      }
 }
 
 // Sum chunk partials in chunk order and finish the family's lp / gradient.
@@ -1259,13 +1263,14 @@ hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, 
     A.qT = ws->qT;
     A.R = ws->R;
     A.Rrows = ws->Rrows;
-    const int njb = (d + G5_BJB - 1) / G5_BJB;
+    const int bjb = g5_bjb(d), njb = (d + bjb - 1) / bjb;
     hipLaunchKernelGGL(k_qt_swizzle, dim3((g5_kp(d) * G5_C + 255) / 256, nsh), dim3(256), 0, st, A, d);
     auto kf = family == STK_LOGREG ? k_gemm_fwd<STK_LOGREG> : k_gemm_fwd<STK_LINREG>;
     if (const hipError_t e = allow_big_lds((const void*)kf)) return e;
     hipLaunchKernelGGL(kf, dim3(nblocks), dim3(64 * G5_FW), lds, st, A);
-    if (const hipError_t e = allow_big_lds((const void*)k_gemm_bwd)) return e;
-    hipLaunchKernelGGL(k_gemm_bwd, dim3(nblocks * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
+    auto kb = bjb == 64 ? k_gemm_bwd<64> : bjb == 128 ? k_gemm_bwd<128> : k_gemm_bwd<256>;
+    if (const hipError_t e = allow_big_lds((const void*)kb)) return e;
+    hipLaunchKernelGGL(kb, dim3(nblocks * njb), dim3(64 * G5_BW), G5_BNS * g5_bstage_bytes(bjb), st, A, njb);
     return hipGetLastError();
   }
   if (family == STK_LOGREG) return pick_c<STK_LOGREG>(A, n, d, T, nblocks, lds, st);

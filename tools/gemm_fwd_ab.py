@@ -4,7 +4,8 @@ writes tools/_bin/gemm_ab_src/gemm_ab.hip -- the product sweep.hip included as i
 pass F frozen in tools/gemm_fwd_r4.hip -- and a harness that checks every pass F arm against
 the product's (lp and gradient after pass B and the chunk reduction) and times them and pass B
 at configs[4]'s shape (d = 1000, 64 chains) on synthetic rows; builds it with hipcc.
-Arms: F (product, 128-row tiles of 4 waves, two blocks per CU), F-w256 (the same kernel with
+Pass B arms: tools/gemm_bwd_r5.hip (wider column blocks, fewer R re-reads).
+Pass F arms: F (product, 128-row tiles of 4 waves, two blocks per CU), F-w256 (the same kernel with
 8 waves: 256-row tiles, one block per CU), F-r4 (round 4: 64-row tiles, 32-column stages).
 Round 5's exploratory variants (8-wave 128-row tiles, pipelined epilogues on 64-row tiles,
 tools/gemm_fwd_r5.hip / gemm_fwd_variants.hip) were built against round 4's sweep.hip.
@@ -18,11 +19,31 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "tools", "_bin", "gemm_ab_src")
 
 
+def ablation_copy(src):
+    """k_gemm_fwd_x<FAM, ABL>: the product pass F with parts removed by text substitution (bit 0:
+    no beta^T LDS-DMA, 1: no X LDS-DMA, 2: the epilogue reduced to folding eta into the lp sum,
+    3: no R stores); ablated arms compute garbage and are timed only."""
+    head = "template <int FAM, int NW = G5_FW>\n__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {"
+    i = src.index(head)
+    j = src.index("\n}\n", i) + 3
+    k = src[i:j].replace(head, "template <int FAM, int ABL, int NW = G5_FW>\n__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd_x(SweepArgs A) {")
+    subs = [("for (int i = 0; i < NDB; ++i) dma16_lds(br,", "for (int i = 0; i < NDB; ++i) if constexpr (!(ABL & 1)) dma16_lds(br,"),
+            ("for (int i = 0; i < NDX; ++i) dma16_lds(xr,", "for (int i = 0; i < NDX; ++i) if constexpr (!(ABL & 2)) dma16_lds(xr,"),
+            ("      if (grow < rcap) *reinterpret_cast<double*>(Rimg", "      if (!(ABL & 8) && grow < rcap) *reinterpret_cast<double*>(Rimg"),
+            ("  auto epi = [&](const int p) {", "  auto epi = [&](const int p) {\n    if constexpr ((ABL & 4) != 0) {\n      const int rt = p / NCT, c2 = p % NCT;\n"
+             "      gaa[c2] += pend[rt][c2][0] + pend[rt][c2][1] + pend[rt][c2][2] + pend[rt][c2][3];\n      return;\n    }")]
+    for a, b in subs:
+        assert k.count(a) == 1, a
+        k = k.replace(a, b)
+    return "namespace stk {\n" + k + "\n}  // namespace stk\n"
+
+
 HARNESS = r'''
 #include <stdarg.h>
 #include <stdio.h>
 #include <vector>
 #include <algorithm>
+#include <string.h>
 void stk_set_error(const char* fmt, ...) { va_list ap; va_start(ap, fmt); vfprintf(stderr, fmt, ap); va_end(ap); fputc('\n', stderr); }
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); exit(1); } } while (0)
 using namespace stk;
@@ -59,17 +80,47 @@ int main(int argc, char** argv) {
   CK(hipStreamSynchronize(st));
   const double flops = 2.0 * rows * nsh * (double)g5_kp(d) * C;
   // kind 0: pass F (par: computes, so checked against F), 1: pass B
-  struct Arm { const char* name; const void* k; int kind; size_t lds; bool par; std::vector<float> ms; int threads; };
+  struct Arm { const char* name; const void* k; int kind; size_t lds; bool par; std::vector<float> ms; int threads; int jb = 0; };
   std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW}};
-  arms.push_back(Arm{"F-w256", (const void*)k_gemm_fwd<STK_LOGREG, 8>, 0, (size_t)G5_FS * (256 * G5_FKC * 8 + G5_FKC * 512) + EX_TAB * 8, true, {}, 512});
+  if (getenv("GEMM_AB_W256")) arms.push_back(Arm{"F-w256", (const void*)k_gemm_fwd<STK_LOGREG, 8>, 0, (size_t)G5_FS * (256 * G5_FKC * 8 + G5_FKC * 512) + EX_TAB * 8, true, {}, 512});
   arms.push_back(Arm{"F-r4", (const void*)k_gemm_fwd_r4<STK_LOGREG>, 0, (size_t)G4_FS * g4_fstage_bytes() + EX_TAB * 8, true, {}, 64 * G4_FW});
-  arms.push_back(Arm{"B", (const void*)k_gemm_bwd, 1, 0, false, {}, 64 * G5_NW});
+  if (getenv("GEMM_AB_ABL")) {
+    arms.push_back(Arm{"F-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 1>, 0, lds, false, {}, 64 * G5_FW});
+    arms.push_back(Arm{"F-noR", (const void*)k_gemm_fwd_x<STK_LOGREG, 8>, 0, lds, false, {}, 64 * G5_FW});
+    arms.push_back(Arm{"F-noEpi", (const void*)k_gemm_fwd_x<STK_LOGREG, 12>, 0, lds, false, {}, 64 * G5_FW});
+    arms.push_back(Arm{"F-noEpiB", (const void*)k_gemm_fwd_x<STK_LOGREG, 13>, 0, lds, false, {}, 64 * G5_FW});
+    arms.push_back(Arm{"F-onlyMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 15>, 0, lds, false, {}, 64 * G5_FW});
+  }
+  arms.push_back(Arm{"B", (const void*)k_gemm_bwd<256>, 3, (size_t)G5_BNS * g5_bstage_bytes(256), true, {}, 64 * G5_BW, 256});
+  // round 4's pass B geometry (128-column blocks of 8 waves, 32-row stages; tools/gemm_bwd_r5.hip)
+  arms.push_back(Arm{"B-r4", (const void*)k_gemm_bwd_w<128, 32, 8, 3>, 3, gemm_bwd_w_lds<128, 32, 8, 3>(), true, {}, 512, 128});
+  // pass B variants (kind 3, tools/gemm_bwd_r5.hip): JB columns x RB rows per stage, NW waves, NS stages
+  if (getenv("GEMM_AB_R5U")) {   // round 5, call u's arms (profiles/r05u_passB_ab_*.log)
+    arms.push_back(Arm{"B-256r16w8s3", (const void*)k_gemm_bwd_w<256, 16, 8, 3>, 3, gemm_bwd_w_lds<256, 16, 8, 3>(), true, {}, 512, 256});
+    arms.push_back(Arm{"B-256r16w8s2", (const void*)k_gemm_bwd_w<256, 16, 8, 2>, 3, gemm_bwd_w_lds<256, 16, 8, 2>(), true, {}, 512, 256});
+    arms.push_back(Arm{"B-256r32w8s2", (const void*)k_gemm_bwd_w<256, 32, 8, 2>, 3, gemm_bwd_w_lds<256, 32, 8, 2>(), true, {}, 512, 256});
+  }
+  arms.push_back(Arm{"B-128r16w4s3", (const void*)k_gemm_bwd_w<128, 16, 4, 3>, 3, gemm_bwd_w_lds<128, 16, 4, 3>(), true, {}, 256, 128});
+  if (getenv("GEMM_AB_R5V")) {   // round 5, call v's arms (profiles/r05v_passB_ab_*.log)
+    arms.push_back(Arm{"B-128r16w4s2", (const void*)k_gemm_bwd_w<128, 16, 4, 2>, 3, gemm_bwd_w_lds<128, 16, 4, 2>(), true, {}, 256, 128});
+    arms.push_back(Arm{"B-128r8w4s4", (const void*)k_gemm_bwd_w<128, 8, 4, 4>, 3, gemm_bwd_w_lds<128, 8, 4, 4>(), true, {}, 256, 128});
+    arms.push_back(Arm{"B-64r16w4s3", (const void*)k_gemm_bwd_w<64, 16, 4, 3>, 3, gemm_bwd_w_lds<64, 16, 4, 3>(), true, {}, 256, 64});
+  }
+  if (getenv("GEMM_AB_R5W")) {   // round 5, call w's arms (profiles/r05w_passB_ab_*.log; 256r8w4s3 is now the product)
+    arms.push_back(Arm{"B-256r16w4s2", (const void*)k_gemm_bwd_w<256, 16, 4, 2>, 3, gemm_bwd_w_lds<256, 16, 4, 2>(), true, {}, 256, 256});
+    arms.push_back(Arm{"B-256r8w4s4", (const void*)k_gemm_bwd_w<256, 8, 4, 4>, 3, gemm_bwd_w_lds<256, 8, 4, 4>(), true, {}, 256, 256});
+  }
+  arms.push_back(Arm{"B-256r8w4s2", (const void*)k_gemm_bwd_w<256, 8, 4, 2>, 3, gemm_bwd_w_lds<256, 8, 4, 2>(), true, {}, 256, 256});
   for (auto& a : arms) CK(hipFuncSetAttribute(a.k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  const int njb = (d + G5_BJB - 1) / G5_BJB;
   auto launch = [&](const Arm& a) {
     if (a.kind == 0) hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs)>(const_cast<void*>(a.k)), dim3(nsh * G), dim3(a.threads), a.lds, st, A);
-    else hipLaunchKernelGGL(k_gemm_bwd, dim3(nsh * G * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
+    else if (a.kind == 3) {
+      const int nj = (d + a.jb - 1) / a.jb;
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(SweepArgs, int)>(const_cast<void*>(a.k)), dim3(nsh * G * nj), dim3(a.threads), a.lds, st, A, nj);
+    }
   };
+  const Arm* prodB = nullptr;
+  for (const Arm& a : arms) if (!strcmp(a.name, "B")) prodB = &a;
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   {   // parity of the arms that compute: pass F + pass B + the chunk reduction
     double *lp, *grad; CK(hipMalloc(&lp, sizeof(double) * nsh * C)); CK(hipMalloc(&grad, sizeof(double) * nsh * C * Dp));
@@ -79,9 +130,14 @@ int main(int argc, char** argv) {
       if (!a.par) continue;
       names.push_back(a.name);
       CK(hipMemset(ws.R, 0xFF, sizeof(double) * (size_t)nsh * ws.Rrows * C));   // NaN: an unwritten R row shows
-      launch(a);
+      if (a.kind == 3) {            // a pass B arm: after the product's pass F
+        launch(arms[0]);
+        launch(a);
+      } else {
+        launch(a);
+        launch(*prodB);
+      }
       CK(hipGetLastError());
-      hipLaunchKernelGGL(k_gemm_bwd, dim3(nsh * G * njb), dim3(64 * G5_NW), G5_BNS * g5_bstage_bytes(), st, A, njb);
       CK(stk_launch_sweep_reduce(STK_LOGREG, sh_d, 0, nsh, d, G, G, q, C, Dp, partial, nullptr, 0, lp, grad, st));
       std::vector<double> h((size_t)nsh * C * (Dp + 1));
       CK(hipMemcpy(h.data(), lp, sizeof(double) * nsh * C, hipMemcpyDeviceToHost));
@@ -93,7 +149,7 @@ int main(int argc, char** argv) {
       for (int i = 0; i < nsh * C; ++i) lpr = std::max(lpr, fabs(res[k][i] - res[0][i]) / fabs(res[0][i]));
       for (size_t i = nsh * C; i < res[0].size(); ++i) gmax = std::max(gmax, fabs(res[0][i]));
       for (size_t i = nsh * C; i < res[0].size(); ++i) gr = std::max(gr, fabs(res[k][i] - res[0][i]) / gmax);
-      printf("parity %s vs F: lp max rel %.3g, grad max |diff| / max|grad| %.3g (lp[0] %.6f)\n", names[k], lpr, gr, res[0][0]);
+      printf("parity %s vs F+B: lp max rel %.3g, grad max |diff| / max|grad| %.3g (lp[0] %.6f)\n", names[k], lpr, gr, res[0][0]);
     }
   }
   printf("rows/shard %lld shards %d d %d C %d: G %d, %.1f GFLOP per pass\n", (long long)rows, nsh, d, C, G, flops / 1e9);
@@ -113,9 +169,11 @@ int main(int argc, char** argv) {
 def main():
     os.makedirs(OUT, exist_ok=True)
     c = os.path.join(ROOT, "stark_amd", "csrc")
+    src = open(os.path.join(c, "sweep.hip")).read()
     body = ('#include "%s"\n#include "%s"\n#include "%s"\n#include "%s"\n'
             % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"), os.path.join(c, "datagen.hip"),
-               os.path.join(ROOT, "tools", "gemm_fwd_r4.hip")) + HARNESS)
+               os.path.join(ROOT, "tools", "gemm_fwd_r4.hip"))
+            + '#include "%s"\n' % os.path.join(ROOT, "tools", "gemm_bwd_r5.hip") + ablation_copy(src) + HARNESS)
     f = os.path.join(OUT, "gemm_ab.hip")
     open(f, "w").write(body)
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", f, "-o",
