@@ -717,16 +717,20 @@ __device__ __forceinline__ void dma16_lds(__amdgpu_buffer_rsrc_t r, char* dst, i
 // Waits: the LDS-DMA loads and the tile's y loads complete in issue order, so "at most the next
 // stage's DMA outstanding" proves the current stage landed whatever the R stores in between do
 // (a store still in flight only makes the count larger).  DESIGN.md section 3.
-template <int FAM, int NW = G5_FW>
+// (Template geometry for tools/gemm_fwd_ab.py's A/B arms: NW waves of RT 16-row tiles, KCF-column
+// stages, an NS-deep ring; the product launches the defaults.)
+template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
-  constexpr int NCT = 4, RT = 2, TR = 32 * NW, KCF = G5_FKC, NS = G5_FS;
+  constexpr int NCT = 4, TR = 16 * RT * NW;
   constexpr int XB = TR * KCF * 8, BB = KCF * 512, STG = XB + BB;
   constexpr int PPR = KCF / 2;                          // 16-B pieces per X row in the stage (8)
   constexpr int NDX = XB / 1024 / NW, NDB = BB / 1024 / NW, NPART = RT * NCT;
-  static_assert(NDX == 4 && NDB >= 1 && BB % (1024 * NW) == 0, "pass F stage geometry");
+  constexpr int FLUSH = 64 / RT;                        // tiles per log1p flush: 256 elements per lane and chain tile
+  static_assert(NDX >= 1 && NDB >= 1 && XB % (1024 * NW) == 0 && BB % (1024 * NW) == 0 && (PPR == 8 || PPR == 16),
+                "pass F stage geometry");
   // X piece swizzle: 128-B rows put rows of one parity on one half of the banks, so XOR the
-  // piece with (row >> 1) & 7 (every A fragment read conflict free)
-  auto swz = [](int row) { return (row >> 1) & 7; };
+  // piece with (row >> 1) & 7; 256-B rows XOR it with row & 15 (every A fragment read conflict free)
+  auto swz = [](int row) { return PPR == 16 ? (row & 15) : ((row >> 1) & 7); };
   const int shard = A.shard0 + blockIdx.x / A.G;
   const int chunk = blockIdx.x % A.G;
   if (A.req_step && A.req_step[shard] != A.step_id - 1) return;
@@ -794,7 +798,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
     const int rt = p / NCT, c2 = p % NCT;                // called from unrolled loops: p is a constant
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int grow = ptile * TR + 32 * w + 16 * rt + lh + 4 * i;   // row of the chunk
+      const int grow = ptile * TR + 16 * RT * w + 16 * rt + lh + 4 * i;   // row of the chunk
       const bool valid = grow < nrows;
       const double eta = pend[rt][c2][i];
       double dv;
@@ -812,7 +816,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
       gaa[c2] += dv;
       if (grow < rcap) *reinterpret_cast<double*>(Rimg + g5_chain_off(grow, 16 * c2 + lr)) = dv;
     }
-    if (FAM == STK_LOGREG && rt == RT - 1 && (ptile & 31) == 31) {   // 32 tiles x 8 elements per lane
+    if (FAM == STK_LOGREG && rt == RT - 1 && (ptile % FLUSH) == FLUSH - 1) {   // FLUSH tiles x 4 RT elements per lane
       lm[c2] -= 2.0 * log1p(sp[c2]);
       sp[c2] = 0.0;
     }
@@ -838,7 +842,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
       for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int64_t grow = (int64_t)(st / NKC) * TR + 32 * w + 16 * rt + lh + 4 * i;
+          const int64_t grow = (int64_t)(st / NKC) * TR + 16 * RT * w + 16 * rt + lh + 4 * i;
           if constexpr (FAM == STK_LOGREG) ybit |= (grow < nrows ? (uint32_t)sh.yi[r0 + grow] & 1u : 0u) << (4 * rt + i);
           else yt[rt][i] = grow < nrows ? sh.y[r0 + grow] : 0.0;
         }
@@ -851,7 +855,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
       double a[RT];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
-        const int r = 32 * w + 16 * rt + lr;
+        const int r = 16 * RT * w + 16 * rt + lr;
         a[rt] = *reinterpret_cast<const double*>(b + r * (16 * PPR) + (((kk >> 1) ^ swz(r)) << 4) + ((kk & 1) << 3));
       }
 #pragma unroll

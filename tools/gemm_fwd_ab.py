@@ -23,10 +23,12 @@ def ablation_copy(src):
     """k_gemm_fwd_x<FAM, ABL>: the product pass F with parts removed by text substitution (bit 0:
     no beta^T LDS-DMA, 1: no X LDS-DMA, 2: the epilogue reduced to folding eta into the lp sum,
     3: no R stores); ablated arms compute garbage and are timed only."""
-    head = "template <int FAM, int NW = G5_FW>\n__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+            "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
-    k = src[i:j].replace(head, "template <int FAM, int ABL, int NW = G5_FW>\n__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd_x(SweepArgs A) {")
+    k = src[i:j].replace(head, "template <int FAM, int ABL, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+                                "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd_x(SweepArgs A) {")
     subs = [("for (int i = 0; i < NDB; ++i) dma16_lds(br,", "for (int i = 0; i < NDB; ++i) if constexpr (!(ABL & 1)) dma16_lds(br,"),
             ("for (int i = 0; i < NDX; ++i) dma16_lds(xr,", "for (int i = 0; i < NDX; ++i) if constexpr (!(ABL & 2)) dma16_lds(xr,"),
             ("      if (grow < rcap) *reinterpret_cast<double*>(Rimg", "      if (!(ABL & 8) && grow < rcap) *reinterpret_cast<double*>(Rimg"),
@@ -82,7 +84,16 @@ int main(int argc, char** argv) {
   // kind 0: pass F (par: computes, so checked against F), 1: pass B
   struct Arm { const char* name; const void* k; int kind; size_t lds; bool par; std::vector<float> ms; int threads; int jb = 0; };
   std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW}};
-  if (getenv("GEMM_AB_W256")) arms.push_back(Arm{"F-w256", (const void*)k_gemm_fwd<STK_LOGREG, 8>, 0, (size_t)G5_FS * (256 * G5_FKC * 8 + G5_FKC * 512) + EX_TAB * 8, true, {}, 512});
+  // pass F geometries: NW waves x RT 16-row tiles per wave, KCF-column stages, NS-deep ring
+#define FARM(NW, RT, KCF, NS) arms.push_back(Arm{"F-" #NW "w" #RT "r" #KCF "k" #NS "s", (const void*)k_gemm_fwd<STK_LOGREG, NW, RT, KCF, NS>, 0, \
+    (size_t)NS * (16 * RT * NW * KCF * 8 + KCF * 512) + EX_TAB * 8, true, {}, 64 * NW})
+  if (getenv("GEMM_AB_R5Y")) {   // round 5, call y's arms (profiles/r05y_passF_geom_*.log)
+    FARM(8, 1, 32, 3);
+    FARM(8, 1, 16, 4);
+    FARM(8, 1, 32, 2);
+    FARM(4, 2, 32, 2);
+    FARM(8, 2, 16, 3);
+  }
   arms.push_back(Arm{"F-r4", (const void*)k_gemm_fwd_r4<STK_LOGREG>, 0, (size_t)G4_FS * g4_fstage_bytes() + EX_TAB * 8, true, {}, 64 * G4_FW});
   if (getenv("GEMM_AB_ABL")) {
     arms.push_back(Arm{"F-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 1>, 0, lds, false, {}, 64 * G5_FW});
