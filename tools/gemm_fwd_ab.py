@@ -22,14 +22,19 @@ OUT = os.path.join(ROOT, "tools", "_bin", "gemm_ab_src")
 def ablation_copy(src):
     """k_gemm_fwd_x<FAM, ABL>: the product pass F with parts removed by text substitution (bit 0:
     no beta^T LDS-DMA, 1: no X LDS-DMA, 2: the epilogue reduced to folding eta into the lp sum,
-    3: no R stores); ablated arms compute garbage and are timed only."""
+    3: no R stores, 4: every tile's X stages read from the chunk's first tile (L2-resident),
+    5: the X stages read as one sequential stream of the same bytes); ablated arms compute
+    garbage and are timed only."""
     head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
     k = src[i:j].replace(head, "template <int FAM, int ABL, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
                                 "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd_x(SweepArgs A) {")
-    subs = [("for (int i = 0; i < NDB; ++i) dma16_lds(br,", "for (int i = 0; i < NDB; ++i) if constexpr (!(ABL & 1)) dma16_lds(br,"),
+    subs = [("    xvo[i] = row * d * 8 + pc * 16;", "    xvo[i] = (ABL & 32) ? row * KCF * 8 + pc * 16 : row * d * 8 + pc * 16;"),
+            ("    const int xso = tile * TR * d * 8 + kc * KCF * 8;",
+             "    const int xso = (ABL & 16) ? kc * KCF * 8 : (ABL & 32) ? st * TR * KCF * 8 : tile * TR * d * 8 + kc * KCF * 8;"),
+            ("for (int i = 0; i < NDB; ++i) dma16_lds(br,", "for (int i = 0; i < NDB; ++i) if constexpr (!(ABL & 1)) dma16_lds(br,"),
             ("for (int i = 0; i < NDX; ++i) dma16_lds(xr,", "for (int i = 0; i < NDX; ++i) if constexpr (!(ABL & 2)) dma16_lds(xr,"),
             ("      if (grow < rcap) *reinterpret_cast<double*>(Rimg", "      if (!(ABL & 8) && grow < rcap) *reinterpret_cast<double*>(Rimg"),
             ("  auto epi = [&](const int p) {", "  auto epi = [&](const int p) {\n    if constexpr ((ABL & 4) != 0) {\n      const int rt = p / NCT, c2 = p % NCT;\n"
@@ -101,6 +106,9 @@ int main(int argc, char** argv) {
     arms.push_back(Arm{"F-noEpi", (const void*)k_gemm_fwd_x<STK_LOGREG, 12>, 0, lds, false, {}, 64 * G5_FW});
     arms.push_back(Arm{"F-noEpiB", (const void*)k_gemm_fwd_x<STK_LOGREG, 13>, 0, lds, false, {}, 64 * G5_FW});
     arms.push_back(Arm{"F-onlyMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 15>, 0, lds, false, {}, 64 * G5_FW});
+    arms.push_back(Arm{"F-Xtile0", (const void*)k_gemm_fwd_x<STK_LOGREG, 16>, 0, lds, false, {}, 64 * G5_FW});
+    arms.push_back(Arm{"F-Xseq", (const void*)k_gemm_fwd_x<STK_LOGREG, 32>, 0, lds, false, {}, 64 * G5_FW});
+    arms.push_back(Arm{"F-Xseq-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 33>, 0, lds, false, {}, 64 * G5_FW});
   }
   arms.push_back(Arm{"B", (const void*)k_gemm_bwd<256>, 3, (size_t)G5_BNS * g5_bstage_bytes(256), true, {}, 64 * G5_BW, 256});
   // round 4's pass B geometry (128-column blocks of 8 waves, 32-row stages; tools/gemm_bwd_r5.hip)
