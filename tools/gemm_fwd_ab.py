@@ -45,6 +45,22 @@ def ablation_copy(src):
     return "namespace stk {\n" + k + "\n}  // namespace stk\n"
 
 
+def early_copy(src):
+    """k_gemm_fwd_e<FAM>: the product pass F with the next stage's DMA issued right after the
+    barrier, before the parked tile's epilogue part and the tile's y loads (the compiler waits
+    for the y loads where it uses them; the DMA'd stages keep their counted waits)."""
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+            "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
+    i = src.index(head)
+    j = src.index("\n}\n", i) + 3
+    k = src[i:j].replace("void k_gemm_fwd(SweepArgs A) {", "void k_gemm_fwd_e(SweepArgs A) {")
+    iss = "    if (st + NS - 1 < nst) issue(st + NS - 1);\n"
+    bar = "    lds_barrier();                                       // stage st landed for every wave; slot of st-1 free\n"
+    assert k.count(iss) == 1 and k.count(bar) == 1
+    k = k.replace(iss, "").replace(bar, bar + iss)
+    return "namespace stk {\n" + k + "\n}  // namespace stk\n"
+
+
 HARNESS = r'''
 #include <stdarg.h>
 #include <stdio.h>
@@ -92,6 +108,7 @@ int main(int argc, char** argv) {
   // pass F geometries: NW waves x RT 16-row tiles per wave, KCF-column stages, NS-deep ring
 #define FARM(NW, RT, KCF, NS) arms.push_back(Arm{"F-" #NW "w" #RT "r" #KCF "k" #NS "s", (const void*)k_gemm_fwd<STK_LOGREG, NW, RT, KCF, NS>, 0, \
     (size_t)NS * (16 * RT * NW * KCF * 8 + KCF * 512) + EX_TAB * 8, true, {}, 64 * NW})
+  arms.push_back(Arm{"F-early", (const void*)k_gemm_fwd_e<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_R5Y")) {   // round 5, call y's arms (profiles/r05y_passF_geom_*.log)
     FARM(8, 1, 32, 3);
     FARM(8, 1, 16, 4);
@@ -192,7 +209,7 @@ def main():
     body = ('#include "%s"\n#include "%s"\n#include "%s"\n#include "%s"\n'
             % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"), os.path.join(c, "datagen.hip"),
                os.path.join(ROOT, "tools", "gemm_fwd_r4.hip"))
-            + '#include "%s"\n' % os.path.join(ROOT, "tools", "gemm_bwd_r5.hip") + ablation_copy(src) + HARNESS)
+            + '#include "%s"\n' % os.path.join(ROOT, "tools", "gemm_bwd_r5.hip") + ablation_copy(src) + early_copy(src) + HARNESS)
     f = os.path.join(OUT, "gemm_ab.hip")
     open(f, "w").write(body)
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", f, "-o",
