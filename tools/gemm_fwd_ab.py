@@ -61,6 +61,24 @@ def early_copy(src):
     return "namespace stk {\n" + k + "\n}  // namespace stk\n"
 
 
+def nt_copies(src):
+    """k_gemm_fwd_n<FAM> / k_gemm_bwd_n<JB>: the product passes with X's LDS-DMA issued
+    non-temporal (aux 2, as k_sweep16's stream: X is read once per pass); beta^T and R keep the
+    default policy (re-read from L2)."""
+    out = "namespace stk {\n__device__ __forceinline__ void dma16_lds_nt(__amdgpu_buffer_rsrc_t r, char* dst, int voff, int soff) {\n" \
+          "  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)dst, 16, voff, soff, 0, 2);\n}\n"
+    for head, name in (("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+                        "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {", ("k_gemm_fwd(", "k_gemm_fwd_n(")),
+                       ("template <int JB>\n__global__ __launch_bounds__(64 * G5_BW, 2) void k_gemm_bwd(SweepArgs A, int njb) {",
+                        ("k_gemm_bwd(", "k_gemm_bwd_n("))):
+        i = src.index(head)
+        j = src.index("\n}\n", i) + 3
+        k = src[i:j].replace(name[0], name[1], 1)
+        assert k.count("dma16_lds(xr,") == 1
+        out += k.replace("dma16_lds(xr,", "dma16_lds_nt(xr,") + "\n"
+    return out + "}  // namespace stk\n"
+
+
 HARNESS = r'''
 #include <stdarg.h>
 #include <stdio.h>
@@ -108,7 +126,8 @@ int main(int argc, char** argv) {
   // pass F geometries: NW waves x RT 16-row tiles per wave, KCF-column stages, NS-deep ring
 #define FARM(NW, RT, KCF, NS) arms.push_back(Arm{"F-" #NW "w" #RT "r" #KCF "k" #NS "s", (const void*)k_gemm_fwd<STK_LOGREG, NW, RT, KCF, NS>, 0, \
     (size_t)NS * (16 * RT * NW * KCF * 8 + KCF * 512) + EX_TAB * 8, true, {}, 64 * NW})
-  arms.push_back(Arm{"F-early", (const void*)k_gemm_fwd_e<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
+  arms.push_back(Arm{"F-ntX", (const void*)k_gemm_fwd_n<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
+  if (getenv("GEMM_AB_EARLY")) arms.push_back(Arm{"F-early", (const void*)k_gemm_fwd_e<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_R5Y")) {   // round 5, call y's arms (profiles/r05y_passF_geom_*.log)
     FARM(8, 1, 32, 3);
     FARM(8, 1, 16, 4);
@@ -128,6 +147,7 @@ int main(int argc, char** argv) {
     arms.push_back(Arm{"F-Xseq-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 33>, 0, lds, false, {}, 64 * G5_FW});
   }
   arms.push_back(Arm{"B", (const void*)k_gemm_bwd<256>, 3, (size_t)G5_BNS * g5_bstage_bytes(256), true, {}, 64 * G5_BW, 256});
+  arms.push_back(Arm{"B-ntX", (const void*)k_gemm_bwd_n<256>, 3, (size_t)G5_BNS * g5_bstage_bytes(256), true, {}, 64 * G5_BW, 256});
   // round 4's pass B geometry (128-column blocks of 8 waves, 32-row stages; tools/gemm_bwd_r5.hip)
   arms.push_back(Arm{"B-r4", (const void*)k_gemm_bwd_w<128, 32, 8, 3>, 3, gemm_bwd_w_lds<128, 32, 8, 3>(), true, {}, 512, 128});
   // pass B variants (kind 3, tools/gemm_bwd_r5.hip): JB columns x RB rows per stage, NW waves, NS stages
@@ -209,7 +229,7 @@ def main():
     body = ('#include "%s"\n#include "%s"\n#include "%s"\n#include "%s"\n'
             % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"), os.path.join(c, "datagen.hip"),
                os.path.join(ROOT, "tools", "gemm_fwd_r4.hip"))
-            + '#include "%s"\n' % os.path.join(ROOT, "tools", "gemm_bwd_r5.hip") + ablation_copy(src) + early_copy(src) + HARNESS)
+            + '#include "%s"\n' % os.path.join(ROOT, "tools", "gemm_bwd_r5.hip") + ablation_copy(src) + early_copy(src) + nt_copies(src) + HARNESS)
     f = os.path.join(OUT, "gemm_ab.hip")
     open(f, "w").write(body)
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", f, "-o",
