@@ -24,6 +24,7 @@ rank processes itself (one per GPU, RCCL) before any GPU call; under a
 launcher (WORLD_SIZE set) --gpus must equal the world size or the run is refused.
 """
 import argparse
+import datetime
 import hashlib
 import json
 import socket
@@ -412,10 +413,13 @@ def main():
         if ndev:
             local_rank %= ndev
             torch.cuda.set_device(local_rank)
+        # ranks other than 0 wait at the final barrier while rank 0 runs the optional sub-records
+        # (up to --deadline-s): a timeout well past that, not the 10-minute default
+        pg_timeout = datetime.timedelta(seconds=max(1800, 3 * a.deadline_s))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=pg_timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=pg_timeout)
     dev = local_rank if ndev else None
     if a.launch_check:
         devs = rank_devices(dist, world, rank, local_rank, dev)
