@@ -124,9 +124,11 @@ int main(int argc, char** argv) {
   struct Arm { const char* name; const void* k; int kind; size_t lds; bool par; std::vector<float> ms; int threads; int jb = 0; };
   std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW}};
   // pass F geometries: NW waves x RT 16-row tiles per wave, KCF-column stages, NS-deep ring
+  // (8-column stages in 4-6 deep rings, 42.7-43.5 ms against 39.5: profiles/r05ae_passF_k8_ab.log,
+  // built with a (row >> 2) & 3 swizzle for 64-B rows, since removed)
 #define FARM(NW, RT, KCF, NS) arms.push_back(Arm{"F-" #NW "w" #RT "r" #KCF "k" #NS "s", (const void*)k_gemm_fwd<STK_LOGREG, NW, RT, KCF, NS>, 0, \
     (size_t)NS * (16 * RT * NW * KCF * 8 + KCF * 512) + EX_TAB * 8, true, {}, 64 * NW})
-  arms.push_back(Arm{"F-ntX", (const void*)k_gemm_fwd_n<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
+  if (getenv("GEMM_AB_NT")) arms.push_back(Arm{"F-ntX", (const void*)k_gemm_fwd_n<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_EARLY")) arms.push_back(Arm{"F-early", (const void*)k_gemm_fwd_e<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_R5Y")) {   // round 5, call y's arms (profiles/r05y_passF_geom_*.log)
     FARM(8, 1, 32, 3);
@@ -147,7 +149,7 @@ int main(int argc, char** argv) {
     arms.push_back(Arm{"F-Xseq-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 33>, 0, lds, false, {}, 64 * G5_FW});
   }
   arms.push_back(Arm{"B", (const void*)k_gemm_bwd<256>, 3, (size_t)G5_BNS * g5_bstage_bytes(256), true, {}, 64 * G5_BW, 256});
-  arms.push_back(Arm{"B-ntX", (const void*)k_gemm_bwd_n<256>, 3, (size_t)G5_BNS * g5_bstage_bytes(256), true, {}, 64 * G5_BW, 256});
+  if (getenv("GEMM_AB_NT")) arms.push_back(Arm{"B-ntX", (const void*)k_gemm_bwd_n<256>, 3, (size_t)G5_BNS * g5_bstage_bytes(256), true, {}, 64 * G5_BW, 256});
   // round 4's pass B geometry (128-column blocks of 8 waves, 32-row stages; tools/gemm_bwd_r5.hip)
   arms.push_back(Arm{"B-r4", (const void*)k_gemm_bwd_w<128, 32, 8, 3>, 3, gemm_bwd_w_lds<128, 32, 8, 3>(), true, {}, 512, 128});
   // pass B variants (kind 3, tools/gemm_bwd_r5.hip): JB columns x RB rows per stage, NW waves, NS stages
