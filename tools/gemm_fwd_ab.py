@@ -79,6 +79,31 @@ def nt_copies(src):
     return out + "}  // namespace stk\n"
 
 
+def spread_copy(src):
+    """k_gemm_fwd_s<FAM>: the product pass F with the next stage's DMA spread over the stage's
+    k-steps (the beta^T pieces and X piece 0 before k-step 0, X piece i before k-step i) instead
+    of all six instructions at once before the MFMAs."""
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+            "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
+    i = src.index(head)
+    j = src.index("\n}\n", i) + 3
+    k = src[i:j].replace("void k_gemm_fwd(SweepArgs A) {", "void k_gemm_fwd_s(SweepArgs A) {")
+    subs = [("  auto issue = [&](int st) {                            // global stage index st = tile * NKC + kc\n",
+             "  auto issue_part = [&](int st, int part) {\n"
+             "    const int tile = st / NKC, kc = st % NKC;\n    char* b = stg + (st % NS) * STG;\n"
+             "    const int xso = tile * TR * d * 8 + kc * KCF * 8;\n"
+             "    if (part == 0) {\n#pragma unroll\n      for (int i = 0; i < NDB; ++i) dma16_lds(br, b + XB + (w * NDB + i) * 1024, lane * 16, kc * KCF * 512 + (w * NDB + i) * 1024);\n    }\n"
+             "    if (part < NDX) dma16_lds(xr, b + (w * NDX + part) * 1024, xvo[part], xso);\n  };\n"
+             "  auto issue = [&](int st) {                            // global stage index st = tile * NKC + kc\n"),
+            ("    if (st + NS - 1 < nst) issue(st + NS - 1);\n", "    const bool doiss = st + NS - 1 < nst;\n"),
+            ("    for (int step = 0; step < KCF / 4; ++step) {\n      const int kk = 4 * step + lh;\n",
+             "    for (int step = 0; step < KCF / 4; ++step) {\n      if (doiss) issue_part(st + NS - 1, step);\n      const int kk = 4 * step + lh;\n")]
+    for a, b2 in subs:
+        assert k.count(a) == 1, a
+        k = k.replace(a, b2)
+    return "namespace stk {\n" + k + "\n}  // namespace stk\n"
+
+
 HARNESS = r'''
 #include <stdarg.h>
 #include <stdio.h>
@@ -129,6 +154,7 @@ int main(int argc, char** argv) {
 #define FARM(NW, RT, KCF, NS) arms.push_back(Arm{"F-" #NW "w" #RT "r" #KCF "k" #NS "s", (const void*)k_gemm_fwd<STK_LOGREG, NW, RT, KCF, NS>, 0, \
     (size_t)NS * (16 * RT * NW * KCF * 8 + KCF * 512) + EX_TAB * 8, true, {}, 64 * NW})
   if (getenv("GEMM_AB_NT")) arms.push_back(Arm{"F-ntX", (const void*)k_gemm_fwd_n<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
+  if (getenv("GEMM_AB_SPREAD")) arms.push_back(Arm{"F-spread", (const void*)k_gemm_fwd_s<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_EARLY")) arms.push_back(Arm{"F-early", (const void*)k_gemm_fwd_e<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_R5Y")) {   // round 5, call y's arms (profiles/r05y_passF_geom_*.log)
     FARM(8, 1, 32, 3);
@@ -231,7 +257,7 @@ def main():
     body = ('#include "%s"\n#include "%s"\n#include "%s"\n#include "%s"\n'
             % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"), os.path.join(c, "datagen.hip"),
                os.path.join(ROOT, "tools", "gemm_fwd_r4.hip"))
-            + '#include "%s"\n' % os.path.join(ROOT, "tools", "gemm_bwd_r5.hip") + ablation_copy(src) + early_copy(src) + nt_copies(src) + HARNESS)
+            + '#include "%s"\n' % os.path.join(ROOT, "tools", "gemm_bwd_r5.hip") + ablation_copy(src) + early_copy(src) + nt_copies(src) + spread_copy(src) + HARNESS)
     f = os.path.join(OUT, "gemm_ab.hip")
     open(f, "w").write(body)
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", f, "-o",
