@@ -1,3 +1,6 @@
+// (Built against stark_amd/csrc/sweep.hip as of commit 2f88366, before round 5 moved the product's
+// pass F to 128-row tiles; it does not build against the current sweep.hip.  Kept as the record of
+// the arms measured in profiles/r05e-r05t and r04o.)
 // Round-5 measurement variant of pass F (stark_amd/csrc/sweep.hip: k_gemm_fwd) for
 // tools/gemm_fwd_ab.py: 128-row tiles shared by 8 waves (one block per CU, two waves per SIMD),
 // each wave 16 rows x all 64 chains -- the product's per-wave shape -- so one beta^T stage feeds

@@ -1,3 +1,6 @@
+// (Built against stark_amd/csrc/sweep.hip as of commit 2f88366, before round 5 moved the product's
+// pass F to 128-row tiles; it does not build against the current sweep.hip.  Kept as the record of
+// the arms measured in profiles/r05e-r05t and r04o.)
 // A/B variants of pass F (sweep.hip: k_gemm_fwd), for tools/gemm_fwd_ab.py.  Included after
 // sweep.hip inside the harness; not part of the library.
 //
