@@ -53,6 +53,9 @@ def test_schools_lpgrad(ctx, orc):
                                    # pass F's stage count per 128-row tile NKC = ceil(d / 16) at 1 and 2 (the
                                    # parked tile's 8 epilogue parts mostly left for the next tile's end)
                                    (300, 16, 64), (300, 17, 64),
+                                   # the largest d the C-ABI takes (1024: 64 pass-F stages per tile, 4 full
+                                   # pass-B column blocks) and one past a pass-B column block
+                                   (200, 1024, 64), (150, 257, 64),
                                    # pass F chunks of > 32 tiles of 128 rows (512 chunks per shard: n > 2.1e6),
                                    # so its residual-v4 running product is flushed inside the loop too
                                    (2200000, 5, 64)])
