@@ -104,6 +104,38 @@ def spread_copy(src):
     return "namespace stk {\n" + k + "\n}  // namespace stk\n"
 
 
+def volatile_copy(src):
+    """k_gemm_fwd_v<FAM>: the product pass F with its A-fragment reads volatile, so the compiler
+    cannot pair a lane's two row tiles (2 KB apart) into one ds_read2st64_b64: that form is
+    serviced in 16-lane groups over 32 banks, where lanes lr and lr ^ 1 of the 128-B X rows
+    share a bank (2-way); as two ds_read_b64 (32-lane groups over 64 banks) they do not."""
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+            "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
+    i = src.index(head)
+    j = src.index("\n}\n", i) + 3
+    k = src[i:j].replace("void k_gemm_fwd(SweepArgs A) {", "void k_gemm_fwd_v(SweepArgs A) {")
+    a = "        a[rt] = *reinterpret_cast<const double*>(b + r * (16 * PPR)"
+    assert k.count(a) == 1
+    k = k.replace(a, "        a[rt] = *reinterpret_cast<const volatile double*>(b + r * (16 * PPR)")
+    return "namespace stk {\n" + k + "\n}  // namespace stk\n"
+
+
+def swz2_copy(src):
+    """k_gemm_fwd_z<FAM>: the product pass F with the X piece swizzle ((row >> 1) & 7) ^ ((row >> 4) & 1):
+    a lane's two row tiles (rows r, r + 16) then sit a lane-dependent distance apart, so the
+    compiler keeps them as two ds_read_b64 (32-lane groups over 64 banks: conflict free) instead
+    of one ds_read2st64_b64 (16-lane groups over 32 banks: lanes lr, lr ^ 1 collide)."""
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+            "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
+    i = src.index(head)
+    j = src.index("\n}\n", i) + 3
+    k = src[i:j].replace("void k_gemm_fwd(SweepArgs A) {", "void k_gemm_fwd_z(SweepArgs A) {")
+    a = "  auto swz = [](int row) { return PPR == 16 ? (row & 15) : ((row >> 1) & 7); };"
+    assert k.count(a) == 1
+    k = k.replace(a, "  auto swz = [](int row) { return PPR == 16 ? (row & 15) : (((row >> 1) & 7) ^ ((row >> 4) & 1)); };")
+    return "namespace stk {\n" + k + "\n}  // namespace stk\n"
+
+
 HARNESS = r'''
 #include <stdarg.h>
 #include <stdio.h>
@@ -154,6 +186,8 @@ int main(int argc, char** argv) {
 #define FARM(NW, RT, KCF, NS) arms.push_back(Arm{"F-" #NW "w" #RT "r" #KCF "k" #NS "s", (const void*)k_gemm_fwd<STK_LOGREG, NW, RT, KCF, NS>, 0, \
     (size_t)NS * (16 * RT * NW * KCF * 8 + KCF * 512) + EX_TAB * 8, true, {}, 64 * NW})
   if (getenv("GEMM_AB_NT")) arms.push_back(Arm{"F-ntX", (const void*)k_gemm_fwd_n<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
+  if (getenv("GEMM_AB_VOLA")) arms.push_back(Arm{"F-volA", (const void*)k_gemm_fwd_v<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
+  if (getenv("GEMM_AB_SWZ2")) arms.push_back(Arm{"F-swz2", (const void*)k_gemm_fwd_z<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_SPREAD")) arms.push_back(Arm{"F-spread", (const void*)k_gemm_fwd_s<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_EARLY")) arms.push_back(Arm{"F-early", (const void*)k_gemm_fwd_e<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_R5Y")) {   // round 5, call y's arms (profiles/r05y_passF_geom_*.log)
@@ -257,7 +291,7 @@ def main():
     body = ('#include "%s"\n#include "%s"\n#include "%s"\n#include "%s"\n'
             % (os.path.join(c, "sweep.hip"), os.path.join(c, "sweep16.hip"), os.path.join(c, "datagen.hip"),
                os.path.join(ROOT, "tools", "gemm_fwd_r4.hip"))
-            + '#include "%s"\n' % os.path.join(ROOT, "tools", "gemm_bwd_r5.hip") + ablation_copy(src) + early_copy(src) + nt_copies(src) + spread_copy(src) + HARNESS)
+            + '#include "%s"\n' % os.path.join(ROOT, "tools", "gemm_bwd_r5.hip") + ablation_copy(src) + early_copy(src) + nt_copies(src) + spread_copy(src) + volatile_copy(src) + swz2_copy(src) + HARNESS)
     f = os.path.join(OUT, "gemm_ab.hip")
     open(f, "w").write(body)
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", f, "-o",

@@ -50,9 +50,13 @@ def main():
         if "SQ_VALU_MFMA_BUSY_CYCLES" in med and "GRBM_GUI_ACTIVE" in med:
             rec["mfma_busy_frac"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / SIMDS / (med["GRBM_GUI_ACTIVE"] / XCDS)
         if "SQ_WAVE_CYCLES" in med:
-            for c in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU"):
+            for c in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY"):
                 if c in med:
                     rec[c.lower() + "_frac_of_wave_cycles"] = med[c] / med["SQ_WAVE_CYCLES"]
+        if "SQ_LDS_BANK_CONFLICT" in med and med.get("SQ_LDS_IDX_ACTIVE"):
+            rec["lds_bank_conflict_frac_of_lds_cycles"] = med["SQ_LDS_BANK_CONFLICT"] / med["SQ_LDS_IDX_ACTIVE"]
+        if "SQ_LDS_IDX_ACTIVE" in med and "GRBM_GUI_ACTIVE" in med:
+            rec["lds_active_frac"] = med["SQ_LDS_IDX_ACTIVE"] / (SIMDS / 4) / (med["GRBM_GUI_ACTIVE"] / XCDS)
         out[k] = rec
     for k, r in sorted(out.items()):
         print(k, " ".join(f"{c}={v:.4g}" for c, v in r.items() if isinstance(v, float) and ("frac" in c or c in ("clock_ghz", "duration_ms"))))
