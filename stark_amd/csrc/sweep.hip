@@ -719,7 +719,7 @@ __device__ __forceinline__ void dma16_lds(__amdgpu_buffer_rsrc_t r, char* dst, i
 // (a store still in flight only makes the count larger).  DESIGN.md section 3.
 // (Template geometry for tools/gemm_fwd_ab.py's A/B arms: NW waves of RT 16-row tiles, KCF-column
 // stages, an NS-deep ring; the product launches the defaults.)
-template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>
+template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
   constexpr int NCT = 4, TR = 16 * RT * NW;
   constexpr int XB = TR * KCF * 8, BB = KCF * 512, STG = XB + BB;
@@ -821,9 +821,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
       sp[c2] = 0.0;
     }
   };
-  for (int st = 0; st < nst; ++st) {
-    const int kc = st % NKC;
-    if (kc == 0) {
+  // One stage: wait for its DMA, barrier, the parked tile's epilogue part(s) due, the tile's y,
+  // the DMA NS - 1 stages ahead, the stage's MFMAs.  part >= 0: that part; -1: none; -2: the
+  // parts p with p % NKC == kc (NKC < NPART); yload: read the tile's y.  Inlined at every call
+  // site with first / part / yload constant where they can be: straight-line steady-state stages.
+  auto stage = [&](const int st, const int kc, const bool first, const int part, const bool yload) {
+    if (first) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -831,12 +834,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
     }
     wait_vmcnt(std::min(NS - 2, nst - 1 - st) * (NDX + NDB));   // own DMAs of stage st retired
     lds_barrier();                                       // stage st landed for every wave; slot of st-1 free
-    if (ptile >= 0) {                                    // the parked tile's parts due at this stage
+    if (part >= 0 && ptile >= 0) epi(part);
+    if (part == -2 && ptile >= 0) {
 #pragma unroll
       for (int p = 0; p < NPART; ++p)
         if (p % NKC == kc) epi(p);
     }
-    if (kc == 0) {                                       // this tile's y (loads: in order with the DMA)
+    if (yload) {                                         // this tile's y (loads: in order with the DMA)
       if constexpr (FAM == STK_LOGREG) ybit = 0u;
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
@@ -865,18 +869,34 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
         for (int rt = 0; rt < RT; ++rt) acc[rt][c2] = mfma_f64(a[rt], bb, acc[rt][c2]);
       }
     }
-    if (kc == NKC - 1) {                                 // park the tile: its epilogue runs during the next
+  };
+  auto park = [&](const int tile) {   // the tile's epilogue runs during the next
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
+    for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
-        for (int c2 = 0; c2 < NCT; ++c2)
+      for (int c2 = 0; c2 < NCT; ++c2)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) pend[rt][c2][i] = acc[rt][c2][i] + alpha[c2];
+        for (int i = 0; i < 4; ++i) pend[rt][c2][i] = acc[rt][c2][i] + alpha[c2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pyt[rt][i] = yt[rt][i];
-      }
-      pybit = ybit;
-      ptile = st / NKC;
+      for (int i = 0; i < 4; ++i) pyt[rt][i] = yt[rt][i];
+    }
+    pybit = ybit;
+    ptile = tile;
+  };
+  if constexpr (SPLIT) {
+    // (NKC >= NPART: the host's choice) tile by tile, the first NPART stages of a tile each carry
+    // one part of the parked tile (p a constant: no per-stage part dispatch), the rest none
+    for (int tile = 0, st = 0; tile < ntile; ++tile, st += NKC) {
+#pragma unroll
+      for (int p = 0; p < NPART; ++p) stage(st + p, p, p == 0, p, p == NPART - 1);   // y after the last part: pend dead
+      for (int kc = NPART; kc < NKC; ++kc) stage(st + kc, kc, false, -1, false);
+      park(tile);
+    }
+  } else {
+    for (int st = 0; st < nst; ++st) {
+      const int kc = st % NKC;
+      stage(st, kc, kc == 0, -2, kc == 0);
+      if (kc == NKC - 1) park(st / NKC);
     }
   }
   if (ptile >= 0) {                                      // the last tile, and any parts NKC < 8 stages left over
@@ -1269,7 +1289,10 @@ hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, 
     A.Rrows = ws->Rrows;
     const int bjb = g5_bjb(d), njb = (d + bjb - 1) / bjb;
     hipLaunchKernelGGL(k_qt_swizzle, dim3((g5_kp(d) * G5_C + 255) / 256, nsh), dim3(256), 0, st, A, d);
-    auto kf = family == STK_LOGREG ? k_gemm_fwd<STK_LOGREG> : k_gemm_fwd<STK_LINREG>;
+    // the split stage schedule needs a tile's NKC = ceil(d / 16) stages to hold its 8 epilogue parts
+    const bool split = (d + G5_FKC - 1) / G5_FKC >= 8;
+    auto kf = family == STK_LOGREG ? (split ? k_gemm_fwd<STK_LOGREG, G5_FW, 2, G5_FKC, G5_FS, true> : k_gemm_fwd<STK_LOGREG>)
+                                   : (split ? k_gemm_fwd<STK_LINREG, G5_FW, 2, G5_FKC, G5_FS, true> : k_gemm_fwd<STK_LINREG>);
     if (const hipError_t e = allow_big_lds((const void*)kf)) return e;
     hipLaunchKernelGGL(kf, dim3(nblocks), dim3(64 * G5_FW), lds, st, A);
     auto kb = bjb == 64 ? k_gemm_bwd<64> : bjb == 128 ? k_gemm_bwd<128> : k_gemm_bwd<256>;

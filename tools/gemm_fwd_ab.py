@@ -5,8 +5,9 @@ pass F frozen in tools/gemm_fwd_r4.hip -- and a harness that checks every pass F
 the product's (lp and gradient after pass B and the chunk reduction) and times them and pass B
 at configs[4]'s shape (d = 1000, 64 chains) on synthetic rows; builds it with hipcc.
 Pass B arms: tools/gemm_bwd_r5.hip (wider column blocks, fewer R re-reads).
-Pass F arms: F (product, 128-row tiles of 4 waves, two blocks per CU), F-w256 (the same kernel with
-8 waves: 256-row tiles, one block per CU), F-r4 (round 4: 64-row tiles, 32-column stages).
+Pass F arms: F (the product at d = 1000: 128-row tiles of 4 waves, two blocks per CU, the split
+stage schedule), F-loop (the same kernel with one epilogue-part dispatch per stage, as used for
+d <= 112), F-r4 (round 4: 64-row tiles, 32-column stages), geometry arms (FARM) and ablations.
 Round 5's exploratory variants (8-wave 128-row tiles, pipelined epilogues on 64-row tiles,
 tools/gemm_fwd_r5.hip / gemm_fwd_variants.hip) were built against round 4's sweep.hip.
 The product source is not changed.
@@ -23,13 +24,14 @@ def ablation_copy(src):
     """k_gemm_fwd_x<FAM, ABL>: the product pass F with parts removed by text substitution (bit 0:
     no beta^T LDS-DMA, 1: no X LDS-DMA, 2: the epilogue reduced to folding eta into the lp sum,
     3: no R stores, 4: every tile's X stages read from the chunk's first tile (L2-resident),
-    5: the X stages read as one sequential stream of the same bytes); ablated arms compute
-    garbage and are timed only."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+    5: the X stages read as one sequential stream of the same bytes, 6: no parked eta at all,
+    the accumulators folded into the gradient sum at the tile's end: 64 VGPRs fewer); ablated
+    arms compute garbage and are timed only."""
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
-    k = src[i:j].replace(head, "template <int FAM, int ABL, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+    k = src[i:j].replace(head, "template <int FAM, int ABL, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
                                 "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd_x(SweepArgs A) {")
     subs = [("    xvo[i] = row * d * 8 + pc * 16;", "    xvo[i] = (ABL & 32) ? row * KCF * 8 + pc * 16 : row * d * 8 + pc * 16;"),
             ("    const int xso = tile * TR * d * 8 + kc * KCF * 8;",
@@ -37,6 +39,9 @@ def ablation_copy(src):
             ("for (int i = 0; i < NDB; ++i) dma16_lds(br,", "for (int i = 0; i < NDB; ++i) if constexpr (!(ABL & 1)) dma16_lds(br,"),
             ("for (int i = 0; i < NDX; ++i) dma16_lds(xr,", "for (int i = 0; i < NDX; ++i) if constexpr (!(ABL & 2)) dma16_lds(xr,"),
             ("      if (grow < rcap) *reinterpret_cast<double*>(Rimg", "      if (!(ABL & 8) && grow < rcap) *reinterpret_cast<double*>(Rimg"),
+            ("        for (int i = 0; i < 4; ++i) pend[rt][c2][i] = acc[rt][c2][i] + alpha[c2];",
+             "        for (int i = 0; i < 4; ++i) { if constexpr ((ABL & 64) != 0) gaa[c2] += acc[rt][c2][i]; else pend[rt][c2][i] = acc[rt][c2][i] + alpha[c2]; }"),
+            ("    ptile = tile;", "    if constexpr (!(ABL & 64)) ptile = tile;"),
             ("  auto epi = [&](const int p) {", "  auto epi = [&](const int p) {\n    if constexpr ((ABL & 4) != 0) {\n      const int rt = p / NCT, c2 = p % NCT;\n"
              "      gaa[c2] += pend[rt][c2][0] + pend[rt][c2][1] + pend[rt][c2][2] + pend[rt][c2][3];\n      return;\n    }")]
     for a, b in subs:
@@ -49,7 +54,7 @@ def early_copy(src):
     """k_gemm_fwd_e<FAM>: the product pass F with the next stage's DMA issued right after the
     barrier, before the parked tile's epilogue part and the tile's y loads (the compiler waits
     for the y loads where it uses them; the DMA'd stages keep their counted waits)."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
@@ -67,7 +72,7 @@ def nt_copies(src):
     default policy (re-read from L2)."""
     out = "namespace stk {\n__device__ __forceinline__ void dma16_lds_nt(__amdgpu_buffer_rsrc_t r, char* dst, int voff, int soff) {\n" \
           "  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)dst, 16, voff, soff, 0, 2);\n}\n"
-    for head, name in (("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+    for head, name in (("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
                         "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {", ("k_gemm_fwd(", "k_gemm_fwd_n(")),
                        ("template <int JB>\n__global__ __launch_bounds__(64 * G5_BW, 2) void k_gemm_bwd(SweepArgs A, int njb) {",
                         ("k_gemm_bwd(", "k_gemm_bwd_n("))):
@@ -83,7 +88,7 @@ def spread_copy(src):
     """k_gemm_fwd_s<FAM>: the product pass F with the next stage's DMA spread over the stage's
     k-steps (the beta^T pieces and X piece 0 before k-step 0, X piece i before k-step i) instead
     of all six instructions at once before the MFMAs."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
@@ -109,7 +114,7 @@ def volatile_copy(src):
     cannot pair a lane's two row tiles (2 KB apart) into one ds_read2st64_b64: that form is
     serviced in 16-lane groups over 32 banks, where lanes lr and lr ^ 1 of the 128-B X rows
     share a bank (2-way); as two ds_read_b64 (32-lane groups over 64 banks) they do not."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
@@ -125,7 +130,7 @@ def swz2_copy(src):
     a lane's two row tiles (rows r, r + 16) then sit a lane-dependent distance apart, so the
     compiler keeps them as two ds_read_b64 (32-lane groups over 64 banks: conflict free) instead
     of one ds_read2st64_b64 (16-lane groups over 32 banks: lanes lr, lr ^ 1 collide)."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS>\n"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
@@ -179,7 +184,9 @@ int main(int argc, char** argv) {
   const double flops = 2.0 * rows * nsh * (double)g5_kp(d) * C;
   // kind 0: pass F (par: computes, so checked against F), 1: pass B
   struct Arm { const char* name; const void* k; int kind; size_t lds; bool par; std::vector<float> ms; int threads; int jb = 0; };
-  std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW}};
+  // the product's pass F at d = 1000: the split stage schedule (stk_launch_sweep picks it for d > 112)
+  std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG, G5_FW, 2, G5_FKC, G5_FS, true>, 0, lds, true, {}, 64 * G5_FW}};
+  arms.push_back(Arm{"F-loop", (const void*)k_gemm_fwd<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   // pass F geometries: NW waves x RT 16-row tiles per wave, KCF-column stages, NS-deep ring
   // (8-column stages in 4-6 deep rings, 42.7-43.5 ms against 39.5: profiles/r05ae_passF_k8_ab.log,
   // built with a (row >> 2) & 3 swizzle for 64-B rows, since removed)
@@ -190,6 +197,7 @@ int main(int argc, char** argv) {
   if (getenv("GEMM_AB_SWZ2")) arms.push_back(Arm{"F-swz2", (const void*)k_gemm_fwd_z<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_SPREAD")) arms.push_back(Arm{"F-spread", (const void*)k_gemm_fwd_s<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_EARLY")) arms.push_back(Arm{"F-early", (const void*)k_gemm_fwd_e<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
+  if (getenv("GEMM_AB_ABL")) arms.push_back(Arm{"F-split-noPark", (const void*)k_gemm_fwd_x<STK_LOGREG, 64, 4, 2, 16, 3, true>, 0, lds, false, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_R5Y")) {   // round 5, call y's arms (profiles/r05y_passF_geom_*.log)
     FARM(8, 1, 32, 3);
     FARM(8, 1, 16, 4);
@@ -204,6 +212,8 @@ int main(int argc, char** argv) {
     arms.push_back(Arm{"F-noEpi", (const void*)k_gemm_fwd_x<STK_LOGREG, 12>, 0, lds, false, {}, 64 * G5_FW});
     arms.push_back(Arm{"F-noEpiB", (const void*)k_gemm_fwd_x<STK_LOGREG, 13>, 0, lds, false, {}, 64 * G5_FW});
     arms.push_back(Arm{"F-onlyMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 15>, 0, lds, false, {}, 64 * G5_FW});
+    arms.push_back(Arm{"F-noPark", (const void*)k_gemm_fwd_x<STK_LOGREG, 64>, 0, lds, false, {}, 64 * G5_FW});
+    arms.push_back(Arm{"F-noPark-onlyMFMA", (const void*)k_gemm_fwd_x<STK_LOGREG, 64 + 15>, 0, lds, false, {}, 64 * G5_FW});
     arms.push_back(Arm{"F-Xtile0", (const void*)k_gemm_fwd_x<STK_LOGREG, 16>, 0, lds, false, {}, 64 * G5_FW});
     arms.push_back(Arm{"F-Xseq", (const void*)k_gemm_fwd_x<STK_LOGREG, 32>, 0, lds, false, {}, 64 * G5_FW});
     arms.push_back(Arm{"F-Xseq-noB", (const void*)k_gemm_fwd_x<STK_LOGREG, 33>, 0, lds, false, {}, 64 * G5_FW});
