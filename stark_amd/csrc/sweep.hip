@@ -719,7 +719,7 @@ __device__ __forceinline__ void dma16_lds(__amdgpu_buffer_rsrc_t r, char* dst, i
 // (a store still in flight only makes the count larger).  DESIGN.md section 3.
 // (Template geometry for tools/gemm_fwd_ab.py's A/B arms: NW waves of RT 16-row tiles, KCF-column
 // stages, an NS-deep ring; the product launches the defaults.)
-template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>
+template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, int SPLIT = 0>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
   constexpr int NCT = 4, TR = 16 * RT * NW;
   constexpr int XB = TR * KCF * 8, BB = KCF * 512, STG = XB + BB;
@@ -883,7 +883,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
     pybit = ybit;
     ptile = tile;
   };
-  if constexpr (SPLIT) {
+  if constexpr (SPLIT == 1) {
     // (NKC >= NPART: the host's choice) tile by tile, the first NPART stages of a tile each carry
     // one part of the parked tile (p a constant: no per-stage part dispatch), the rest none
     for (int tile = 0, st = 0; tile < ntile; ++tile, st += NKC) {
@@ -1291,8 +1291,8 @@ hipError_t stk_launch_sweep(int family, const ShardDev* shards_dev, int shard0, 
     hipLaunchKernelGGL(k_qt_swizzle, dim3((g5_kp(d) * G5_C + 255) / 256, nsh), dim3(256), 0, st, A, d);
     // the split stage schedule needs a tile's NKC = ceil(d / 16) stages to hold its 8 epilogue parts
     const bool split = (d + G5_FKC - 1) / G5_FKC >= 8;
-    auto kf = family == STK_LOGREG ? (split ? k_gemm_fwd<STK_LOGREG, G5_FW, 2, G5_FKC, G5_FS, true> : k_gemm_fwd<STK_LOGREG>)
-                                   : (split ? k_gemm_fwd<STK_LINREG, G5_FW, 2, G5_FKC, G5_FS, true> : k_gemm_fwd<STK_LINREG>);
+    auto kf = family == STK_LOGREG ? (split ? k_gemm_fwd<STK_LOGREG, G5_FW, 2, G5_FKC, G5_FS, 1> : k_gemm_fwd<STK_LOGREG>)
+                                   : (split ? k_gemm_fwd<STK_LINREG, G5_FW, 2, G5_FKC, G5_FS, 1> : k_gemm_fwd<STK_LINREG>);
     if (const hipError_t e = allow_big_lds((const void*)kf)) return e;
     hipLaunchKernelGGL(kf, dim3(nblocks), dim3(64 * G5_FW), lds, st, A);
     auto kb = bjb == 64 ? k_gemm_bwd<64> : bjb == 128 ? k_gemm_bwd<128> : k_gemm_bwd<256>;

@@ -27,11 +27,11 @@ def ablation_copy(src):
     5: the X stages read as one sequential stream of the same bytes, 6: no parked eta at all,
     the accumulators folded into the gradient sum at the tile's end: 64 VGPRs fewer); ablated
     arms compute garbage and are timed only."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, int SPLIT = 0>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
-    k = src[i:j].replace(head, "template <int FAM, int ABL, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
+    k = src[i:j].replace(head, "template <int FAM, int ABL, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, int SPLIT = 0>\n"
                                 "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd_x(SweepArgs A) {")
     subs = [("    xvo[i] = row * d * 8 + pc * 16;", "    xvo[i] = (ABL & 32) ? row * KCF * 8 + pc * 16 : row * d * 8 + pc * 16;"),
             ("    const int xso = tile * TR * d * 8 + kc * KCF * 8;",
@@ -54,7 +54,7 @@ def early_copy(src):
     """k_gemm_fwd_e<FAM>: the product pass F with the next stage's DMA issued right after the
     barrier, before the parked tile's epilogue part and the tile's y loads (the compiler waits
     for the y loads where it uses them; the DMA'd stages keep their counted waits)."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, int SPLIT = 0>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
@@ -72,7 +72,7 @@ def nt_copies(src):
     default policy (re-read from L2)."""
     out = "namespace stk {\n__device__ __forceinline__ void dma16_lds_nt(__amdgpu_buffer_rsrc_t r, char* dst, int voff, int soff) {\n" \
           "  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)dst, 16, voff, soff, 0, 2);\n}\n"
-    for head, name in (("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
+    for head, name in (("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, int SPLIT = 0>\n"
                         "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {", ("k_gemm_fwd(", "k_gemm_fwd_n(")),
                        ("template <int JB>\n__global__ __launch_bounds__(64 * G5_BW, 2) void k_gemm_bwd(SweepArgs A, int njb) {",
                         ("k_gemm_bwd(", "k_gemm_bwd_n("))):
@@ -88,7 +88,7 @@ def spread_copy(src):
     """k_gemm_fwd_s<FAM>: the product pass F with the next stage's DMA spread over the stage's
     k-steps (the beta^T pieces and X piece 0 before k-step 0, X piece i before k-step i) instead
     of all six instructions at once before the MFMAs."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, int SPLIT = 0>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
@@ -114,7 +114,7 @@ def volatile_copy(src):
     cannot pair a lane's two row tiles (2 KB apart) into one ds_read2st64_b64: that form is
     serviced in 16-lane groups over 32 banks, where lanes lr and lr ^ 1 of the 128-B X rows
     share a bank (2-way); as two ds_read_b64 (32-lane groups over 64 banks) they do not."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, int SPLIT = 0>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
@@ -130,7 +130,7 @@ def swz2_copy(src):
     a lane's two row tiles (rows r, r + 16) then sit a lane-dependent distance apart, so the
     compiler keeps them as two ds_read_b64 (32-lane groups over 64 banks: conflict free) instead
     of one ds_read2st64_b64 (16-lane groups over 32 banks: lanes lr, lr ^ 1 collide)."""
-    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, bool SPLIT = false>\n"
+    head = ("template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, int SPLIT = 0>\n"
             "__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {")
     i = src.index(head)
     j = src.index("\n}\n", i) + 3
@@ -185,8 +185,10 @@ int main(int argc, char** argv) {
   // kind 0: pass F (par: computes, so checked against F), 1: pass B
   struct Arm { const char* name; const void* k; int kind; size_t lds; bool par; std::vector<float> ms; int threads; int jb = 0; };
   // the product's pass F at d = 1000: the split stage schedule (stk_launch_sweep picks it for d > 112)
-  std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG, G5_FW, 2, G5_FKC, G5_FS, true>, 0, lds, true, {}, 64 * G5_FW}};
+  std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG, G5_FW, 2, G5_FKC, G5_FS, 1>, 0, lds, true, {}, 64 * G5_FW}};
   arms.push_back(Arm{"F-loop", (const void*)k_gemm_fwd<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
+  // (the parts spread over the tile, part p at stage p NKC / 8: 40.05 / 62.86 ms against the split
+  // head's 39.75 / 62.15, profiles/r05ap_*; its SPLIT = 2 schedule since removed)
   // pass F geometries: NW waves x RT 16-row tiles per wave, KCF-column stages, NS-deep ring
   // (8-column stages in 4-6 deep rings, 42.7-43.5 ms against 39.5: profiles/r05ae_passF_k8_ab.log,
   // built with a (row >> 2) & 3 swizzle for 64-B rows, since removed)
@@ -197,7 +199,7 @@ int main(int argc, char** argv) {
   if (getenv("GEMM_AB_SWZ2")) arms.push_back(Arm{"F-swz2", (const void*)k_gemm_fwd_z<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_SPREAD")) arms.push_back(Arm{"F-spread", (const void*)k_gemm_fwd_s<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_EARLY")) arms.push_back(Arm{"F-early", (const void*)k_gemm_fwd_e<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
-  if (getenv("GEMM_AB_ABL")) arms.push_back(Arm{"F-split-noPark", (const void*)k_gemm_fwd_x<STK_LOGREG, 64, 4, 2, 16, 3, true>, 0, lds, false, {}, 64 * G5_FW});
+  if (getenv("GEMM_AB_ABL")) arms.push_back(Arm{"F-split-noPark", (const void*)k_gemm_fwd_x<STK_LOGREG, 64, 4, 2, 16, 3, 1>, 0, lds, false, {}, 64 * G5_FW});
   if (getenv("GEMM_AB_R5Y")) {   // round 5, call y's arms (profiles/r05y_passF_geom_*.log)
     FARM(8, 1, 32, 3);
     FARM(8, 1, 16, 4);
