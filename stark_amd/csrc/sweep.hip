@@ -712,13 +712,16 @@ __device__ __forceinline__ void dma16_lds(__amdgpu_buffer_rsrc_t r, char* dst, i
 // (LDS-DMA volume 1.5 x the X bytes; round 4's 64-row tiles: 2 x).  Two blocks per CU (72 KB of
 // LDS each with the exp table) overlap one block's epilogue with the other's MFMAs.  The 64
 // accumulators per lane leave no room for the whole tile's epilogue at once, so it is
-// pipelined: the finished tile's eta is parked, and one (row tile, chain tile) part of 4
-// elements is done per stage of the next tile (all 8 at the chunk's end if NKC < 8).
+// pipelined: the finished tile's eta is parked, and its 8 (row tile, chain tile) parts of 4
+// elements are done during the next tile.  SPLIT = 1 (the product for d > 112, NKC >= 8): the
+// next tile's first 8 stages are unrolled, each carrying one part as a compile-time constant,
+// then a plain loop over the rest -- no per-stage part dispatch, which cost 3-5 % (DESIGN.md
+// section 3); SPLIT = 0: the parts p with p % NKC == kc at stage kc (the rest at the chunk's end).
 // Waits: the LDS-DMA loads and the tile's y loads complete in issue order, so "at most the next
 // stage's DMA outstanding" proves the current stage landed whatever the R stores in between do
 // (a store still in flight only makes the count larger).  DESIGN.md section 3.
 // (Template geometry for tools/gemm_fwd_ab.py's A/B arms: NW waves of RT 16-row tiles, KCF-column
-// stages, an NS-deep ring; the product launches the defaults.)
+// stages, an NS-deep ring; the product launches the defaults with SPLIT 0 or 1.)
 template <int FAM, int NW = G5_FW, int RT = 2, int KCF = G5_FKC, int NS = G5_FS, int SPLIT = 0>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_fwd(SweepArgs A) {
   constexpr int NCT = 4, TR = 16 * RT * NW;
