@@ -187,6 +187,8 @@ int main(int argc, char** argv) {
   // the product's pass F at d = 1000: the split stage schedule (stk_launch_sweep picks it for d > 112)
   std::vector<Arm> arms = {{"F", (const void*)k_gemm_fwd<STK_LOGREG, G5_FW, 2, G5_FKC, G5_FS, 1>, 0, lds, true, {}, 64 * G5_FW}};
   arms.push_back(Arm{"F-loop", (const void*)k_gemm_fwd<STK_LOGREG>, 0, lds, true, {}, 64 * G5_FW});
+  // (alpha re-read at the park instead of held, 1 VGPR spilled instead of 4: 38.70 / 60.66 ms against
+  // 38.44 / 60.39, profiles/r05as_*; its SPLIT = 3 form since removed)
   // (the parts spread over the tile, part p at stage p NKC / 8: 40.05 / 62.86 ms against the split
   // head's 39.75 / 62.15, profiles/r05ap_*; its SPLIT = 2 schedule since removed)
   // pass F geometries: NW waves x RT 16-row tiles per wave, KCF-column stages, NS-deep ring
