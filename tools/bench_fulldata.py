@@ -12,8 +12,9 @@ state-machine step.  Timed: K steps after W untimed ones, from the start of samp
 costs the same whatever the sampler phase, and a config-4 chain needs far more than a bench
 window of full-data gradients to adapt, so ESS/s is not reported for this config).
 
-Usage: python tools/bench_fulldata.py [--rows-per-gpu R --steps K --warmup W];
-       N GPUs: python -m torch.distributed.run --nproc-per-node N tools/bench_fulldata.py ...
+Usage: python tools/bench_fulldata.py [--gpus N --rows-per-gpu R --steps K --warmup W]: --gpus N > 1
+starts N rank processes itself with bench.py's launcher (one per GPU, before any GPU call).
+bench.py runs `run()` on every rank of its own N-rank job (its configs4_fulldata sub-record).
 """
 import argparse
 import json
@@ -51,9 +52,10 @@ def run(rows, d=1000, chains=64, steps=30, warmup=3, seed=20240, init_radius=2.0
     A = adapt_iters
     nw = A if A > 0 else 1000
     total = nw + K + W + 1
+    # save_warmup: the chain positions of every transition, the fingerprint compared across ranks
     fs = fulldata.FullDataSampler(model, num_warmup=nw, num_samples=total - nw, chains=chains, seed=seed + 1,
                                   stepsize_jitter=0.5 if A > 0 else 0.0, init_radius=init_radius,
-                                  nuts_criterion=nuts_criterion)
+                                  nuts_criterion=nuts_criterion, save_warmup=True)
     if rank == 0:
         print(f"[bench_fulldata] {world} GPU(s) x {rows} rows x d={d}: {model.device_bytes() / 1e9:.1f} GB/GPU, "
               f"generated in {t_gen:.1f}s", file=sys.stderr, flush=True)
@@ -103,10 +105,22 @@ def run(rows, d=1000, chains=64, steps=30, warmup=3, seed=20240, init_radius=2.0
                 seg = dr[:-1, c * per + f0: c * per + f0 + done[c]]
                 es += np.array([diagnostics.ess(seg[j]) for j in range(seg.shape[0])])
         min_ess = float(np.nanmin(es)) if es.any() else None
+    # every rank runs the same chains on the all-reduced gradients: their positions (warmup
+    # included), step sizes and iteration counts must agree bit for bit on every rank
+    import hashlib
+    eps, im = fs.adaptation()
+    h = hashlib.sha256()
+    for arr in (fs.unconstrained(0), eps, im, it1):
+        h.update(np.ascontiguousarray(arr).tobytes())
+    fp = np.zeros(world)
+    fp[rank] = int(h.hexdigest()[:12], 16)              # 48 bits: exact in fp64
     if world > 1:
         v = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local_rank))
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         elapsed = float(v.item())
+        f = torch.from_numpy(fp).to(torch.device("cuda", local_rank))
+        dist.all_reduce(f)
+        fp = f.cpu().numpy()
     if min_ess:
         ess_ps = min_ess / elapsed
     nsteps = i1["steps"] - i0["steps"]
@@ -138,6 +152,7 @@ def run(rows, d=1000, chains=64, steps=30, warmup=3, seed=20240, init_radius=2.0
                      "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
                              "algorithmic_bytes_per_launch": hbm_bytes}},
         "setup_s": {"datagen": t_gen, "adaptation": t_adapt},
+        "chains_sha16_per_rank": [f"{int(v):012x}" for v in fp],
     }
     fs.close()
     model.close()
@@ -146,6 +161,7 @@ def run(rows, d=1000, chains=64, steps=30, warmup=3, seed=20240, init_radius=2.0
 
 def main():
     p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); > 1 without a launcher: spawned here")
     p.add_argument("--rows-per-gpu", type=float, default=2.5e7)
     p.add_argument("--d", type=int, default=1000)
     p.add_argument("--chains", type=int, default=64)
@@ -158,12 +174,21 @@ def main():
                    help="> 0: run Stan's warmup (untimed) first and report ESS/s of the transitions the "
                         "chains complete inside the timed window")
     a = p.parse_args()
+    import bench
+    refuse = bench.check_world(a.gpus, os.environ)
+    if refuse:
+        sys.exit(refuse)
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        sys.exit(bench.launch_ranks(a.gpus, sys.argv[1:], script=__file__))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     # STARK_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N-rank path on one
     # GPU (ranks share devices round-robin); the driver's runs use RCCL, one rank per GPU
     backend = os.environ.get("STARK_DIST_BACKEND", "nccl")
     import torch
     import torch.distributed as dist
+    refuse = bench.check_devices(backend, os.environ, torch.cuda.device_count())
+    if refuse:
+        sys.exit(refuse)
     local_rank = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     if world > 1:
