@@ -407,9 +407,16 @@ class Ranks:
         if self.dist:
             self.dist.barrier()
 
-    def log(self, msg):
-        if self.rank == 0:
-            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+    def log(self, msg, every_s=0.0):
+        """rank 0 -> stderr; every_s > 0: a progress line, printed at most once per every_s seconds
+        (the driver keeps only the tail of stdout + stderr: the line must not be pushed out of it)."""
+        if self.rank != 0:
+            return
+        now = time.monotonic()
+        if every_s and now - getattr(self, "_last", -1e9) < every_s:
+            return
+        self._last = now
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def rank_devices(R):
@@ -509,7 +516,7 @@ def consensus_job(a, R, ctx, left, cpu_seconds=None):
         sampler.run(A, max_steps=1000)
         its = sampler.iterations()
         R.log(f"{tag} warmup {time.perf_counter() - t:.0f}s: transitions min/median {its.min()}/{int(np.median(its))}"
-              f" of {A}")
+              f" of {A}", every_s=30)
         if its.min() >= A:
             break
     t_adapt = time.perf_counter() - t
@@ -567,7 +574,7 @@ def consensus_job(a, R, ctx, left, cpu_seconds=None):
     while True:                      # bounded batches with a progress line (long phases under the 2.19 criterion)
         sampler.run(A + n_post, max_steps=2000)
         its = sampler.iterations()
-        R.log(f"{tag} draws {time.perf_counter() - t:.0f}s: post-warmup min {its.min() - A} of {n_post}")
+        R.log(f"{tag} draws {time.perf_counter() - t:.0f}s: post-warmup min {its.min() - A} of {n_post}", every_s=30)
         if its.min() >= A + n_post:
             break
         if a.ess_budget_s is not None and time.perf_counter() - t > a.ess_budget_s:
@@ -726,7 +733,7 @@ def _second_run(a, R, ctx, model, shard_ids, gather_ids, A, left):
             done = R.agree(its.min() >= target)
             over = not R.agree(not (time.perf_counter() - t > a.second_budget_s or left() < 150))
             R.log(f"second criterion {a.second_criterion}: {time.perf_counter() - t:.0f}s, transitions min "
-                  f"{its.min()} of {target}")
+                  f"{its.min()} of {target}", every_s=30)
             if done or over:
                 break
         ctx.sync()

@@ -178,6 +178,19 @@ STK_API int stk_sampler_adaptation(stk_sampler* s, double* stepsize, double* inv
 STK_API int stk_sampler_iterations(stk_sampler* s, int32_t* iters);
 STK_API int stk_sampler_destroy(stk_sampler* s);
 
+/* ---- checkpoint / resume of a run between stk_sampler_run calls.  The state is every chain's
+ * device state (position, momentum, gradient, tree stack, adaptation windows and dual-averaging
+ * scalars, Philox counters, mode and iteration), the draws and stats so far and the pending
+ * evaluation requests, plus the step counters: a run saved after any stk_sampler_run call and
+ * loaded into a sampler created from the same model geometry and config -- in another process,
+ * on another device -- continues bit for bit as the unsplit run would (the reference has no
+ * counterpart: a pystan fit cannot be resumed; SURVEY.md 8 aux "checkpoint/resume").
+ * stk_sampler_state_bytes gives the size of the blob; stk_sampler_load_state refuses a blob
+ * of another geometry / config (STK_E_ARG) before writing anything. */
+STK_API int stk_sampler_state_bytes(stk_sampler* s, int64_t* bytes);
+STK_API int stk_sampler_save_state(stk_sampler* s, void* buf, int64_t bytes);
+STK_API int stk_sampler_load_state(stk_sampler* s, const void* buf, int64_t bytes);
+
 /* ---- full-data mode (BASELINE configs[4]): ONE posterior whose rows are split over ranks.
  * Every rank builds a one-shard model of its rows and a sampler with the same config and the
  * same shard_ids (so the chains' RNG streams agree); after each step's local sweep + reduce,

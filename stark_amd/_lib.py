@@ -93,6 +93,9 @@ SIGNATURES = [
     ("stk_sampler_adaptation", ctypes.c_int, [_vp, _vp, _vp]),
     ("stk_sampler_iterations", ctypes.c_int, [_vp, _vp]),
     ("stk_sampler_destroy", ctypes.c_int, [_vp]),
+    ("stk_sampler_state_bytes", ctypes.c_int, [_vp, ctypes.POINTER(_i64)]),
+    ("stk_sampler_save_state", ctypes.c_int, [_vp, _vp, _i64]),
+    ("stk_sampler_load_state", ctypes.c_int, [_vp, _vp, _i64]),
     ("stk_sampler_grad_block", ctypes.c_int, [_vp, ctypes.POINTER(_i64)]),
     ("stk_sampler_set_allreduce", ctypes.c_int, [_vp, _vp, _vp, _vp]),
     ("stk_sample", ctypes.c_int, [_vp, ctypes.POINTER(Config), _vp, _vp, ctypes.POINTER(RunInfo)]),

@@ -932,6 +932,149 @@ int stk_sampler_iterations(stk_sampler* s, int32_t* iters) {
   return STK_OK;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------- checkpoint / resume
+// Blob: StateHeader, then the device segments in state_segments() order.  The header's
+// geometry hash covers everything that shapes the state or its evolution (model family and
+// shard geometry, priors, every sampler setting, the RNG seed and shard ids), so a blob only
+// loads into a sampler that continues the same run.
+namespace {
+struct StateHeader {
+  char magic[8];
+  uint32_t version, nsegs;
+  uint64_t geometry;
+  int64_t step, steps, sweeps, shard_sweeps;
+  double sweep_ms;
+  uint64_t seg_bytes[16];
+};
+struct Seg {
+  void* p;
+  size_t bytes;
+};
+const char kStateMagic[8] = {'S', 'T', 'K', 'S', 'T', 'A', 'T', 'E'};
+
+std::vector<Seg> state_segments(const stk_sampler* s) {
+  const NutsArgs& A = s->A;
+  const size_t n = (size_t)A.nchains, Dp = (size_t)A.Dp, md = (size_t)A.max_depth;
+  const size_t nsh = (size_t)s->m->nshards, S = (size_t)A.S_total;
+  return {{A.vec, sizeof(double) * n * V_COUNT * Dp},
+          {A.stk, sizeof(double) * n * md * SV_COUNT * Dp},
+          {A.sc, sizeof(double) * n * S_COUNT},
+          {A.stks, sizeof(double) * n * md * SS_COUNT},
+          {A.iv, sizeof(int) * n * I_COUNT},
+          {A.cnt, sizeof(unsigned long long) * n * C_COUNT},
+          {A.qeval, sizeof(double) * n * Dp},
+          {A.g_in, sizeof(double) * (n * Dp + n)},       // [grad | lp] at the pending requests
+          {A.draws, sizeof(double) * nsh * s->m->Pmax * S},
+          {A.stats, sizeof(double) * nsh * S * N_STATS},
+          {A.udraws, sizeof(double) * n * (size_t)A.ud_iters * Dp},
+          {A.req_step, sizeof(int) * nsh}};
+}
+
+struct Fnv {
+  uint64_t h = 1469598103934665603ull;
+  template <class T>
+  void add(const T& v) {
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(&v);
+    for (size_t i = 0; i < sizeof(T); ++i) h = (h ^ b[i]) * 1099511628211ull;
+  }
+};
+
+int state_geometry(const stk_sampler* s, uint64_t* out) {
+  const NutsArgs& A = s->A;
+  const stk_model* m = s->m;
+  Fnv f;
+  f.add(m->family), f.add(m->nshards), f.add(m->d), f.add(m->Dmax), f.add(m->Pmax);
+  for (const auto& sd : m->sh) f.add(sd.n), f.add(sd.D), f.add(sd.P), f.add(sd.pa), f.add(sd.pb);
+  f.add(A.nchains), f.add(A.C), f.add(A.Dp), f.add(A.max_depth), f.add(A.num_warmup), f.add(A.num_samples);
+  f.add(A.adapt), f.add(A.var_on), f.add(A.skip_ss), f.add(A.iter_offset);
+  f.add(A.init_buffer), f.add(A.term_buffer), f.add(A.base_window);
+  f.add(A.delta), f.add(A.gamma), f.add(A.kappa), f.add(A.t0), f.add(A.seed), f.add(A.jitter);
+  f.add(A.uturn_ext), f.add(A.cpw_cap), f.add(A.ud_first), f.add(A.ud_iters), f.add(s->nch);
+  std::vector<int32_t> ids(m->nshards);
+  for (int i = 0; i < m->nshards; ++i) ids[i] = i;
+  if (A.shard_ids)
+    STK_HIP_CHECK(hipMemcpy(ids.data(), A.shard_ids, sizeof(int32_t) * ids.size(), hipMemcpyDeviceToHost));
+  for (int v : ids) f.add(v);
+  *out = f.h;
+  return STK_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int stk_sampler_state_bytes(stk_sampler* s, int64_t* bytes) {
+  ARG_CHECK(s && bytes, "stk_sampler_state_bytes: bad arguments");
+  size_t n = sizeof(StateHeader);
+  for (const Seg& g : state_segments(s)) n += g.bytes;
+  *bytes = (int64_t)n;
+  return STK_OK;
+}
+
+int stk_sampler_save_state(stk_sampler* s, void* buf, int64_t bytes) {
+  ARG_CHECK(s && buf, "stk_sampler_save_state: bad arguments");
+  int64_t need = 0;
+  RC(stk_sampler_state_bytes(s, &need));
+  ARG_CHECK(bytes >= need, "stk_sampler_save_state: buffer of %lld bytes, the state needs %lld", (long long)bytes,
+            (long long)need);
+  stk_ctx* ctx = s->m->ctx;
+  STK_HIP_CHECK(hipSetDevice(ctx->device));
+  const auto segs = state_segments(s);
+  StateHeader h{};
+  memcpy(h.magic, kStateMagic, 8);
+  h.version = 1;
+  h.nsegs = (uint32_t)segs.size();
+  RC(state_geometry(s, &h.geometry));
+  h.step = s->step;
+  h.steps = s->steps;
+  h.sweeps = s->sweeps;
+  h.shard_sweeps = s->shard_sweeps;
+  h.sweep_ms = s->sweep_ms;
+  for (size_t i = 0; i < segs.size(); ++i) h.seg_bytes[i] = segs[i].bytes;
+  char* out = static_cast<char*>(buf);
+  memcpy(out, &h, sizeof(h));
+  size_t off = sizeof(h);
+  for (const Seg& g : segs) {
+    STK_HIP_CHECK(hipMemcpyAsync(out + off, g.p, g.bytes, hipMemcpyDefault, ctx->stream));
+    off += g.bytes;
+  }
+  STK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  return STK_OK;
+}
+
+int stk_sampler_load_state(stk_sampler* s, const void* buf, int64_t bytes) {
+  ARG_CHECK(s && buf, "stk_sampler_load_state: bad arguments");
+  int64_t need = 0;
+  RC(stk_sampler_state_bytes(s, &need));
+  ARG_CHECK(bytes == need, "stk_sampler_load_state: blob of %lld bytes, this sampler's state has %lld",
+            (long long)bytes, (long long)need);
+  stk_ctx* ctx = s->m->ctx;
+  STK_HIP_CHECK(hipSetDevice(ctx->device));
+  StateHeader h;
+  memcpy(&h, buf, sizeof(h));
+  const auto segs = state_segments(s);
+  uint64_t geo = 0;
+  RC(state_geometry(s, &geo));
+  ARG_CHECK(!memcmp(h.magic, kStateMagic, 8) && h.version == 1, "stk_sampler_load_state: not a sampler state blob");
+  ARG_CHECK(h.geometry == geo && h.nsegs == segs.size(),
+            "stk_sampler_load_state: the state belongs to another model geometry or sampler config");
+  for (size_t i = 0; i < segs.size(); ++i)
+    ARG_CHECK(h.seg_bytes[i] == segs[i].bytes, "stk_sampler_load_state: segment %zu size mismatch", i);
+  const char* in = static_cast<const char*>(buf) + sizeof(h);
+  for (const Seg& g : segs) {
+    STK_HIP_CHECK(hipMemcpyAsync(g.p, in, g.bytes, hipMemcpyDefault, ctx->stream));
+    in += g.bytes;
+  }
+  STK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  s->step = (int)h.step;
+  s->steps = h.steps;
+  s->sweeps = h.sweeps;
+  s->shard_sweeps = h.shard_sweeps;
+  s->sweep_ms = h.sweep_ms;
+  return STK_OK;
+}
+
 int stk_sample(stk_model* m, const stk_config* cfg, double* draws, double* stats, stk_run_info* info) {
   stk_sampler* s = nullptr;
   RC(stk_sampler_create(m, cfg, &s));

@@ -345,6 +345,25 @@ class Sampler:
                                                     ctypes.c_void_p(block_ptr) if block_ptr else None))
         return self
 
+    def save_state(self) -> np.ndarray:
+        """The run so far as a byte blob (uint8 array): every chain's device state, the draws
+        and the step counters (stk_sampler_save_state).  load_state() of the blob into a sampler
+        of the same model geometry and config -- in another process, on another GPU --
+        continues the run bit for bit as if it had never stopped."""
+        n = ctypes.c_int64()
+        lib = _lib.load()
+        check(lib.stk_sampler_state_bytes(self._h, ctypes.byref(n)))
+        buf = np.empty(n.value, np.uint8)
+        check(lib.stk_sampler_save_state(self._h, buf.ctypes.data, n.value))
+        return buf
+
+    def load_state(self, blob) -> "Sampler":
+        """Resume a run saved by save_state() (raises StarkHipError on another geometry / config)."""
+        buf = np.ascontiguousarray(np.frombuffer(blob, np.uint8) if isinstance(blob, (bytes, bytearray)) else blob,
+                                   np.uint8)
+        check(_lib.load().stk_sampler_load_state(self._h, buf.ctypes.data, buf.size))
+        return self
+
     def info(self) -> dict:
         ri = RunInfo()
         check(_lib.load().stk_sampler_info(self._h, ctypes.byref(ri)))

@@ -245,6 +245,83 @@ def test_bitwise_reproducible_and_resumable(ctx, C):
     b.close()
 
 
+_SAVE_SCRIPT = """
+import sys
+sys.path.insert(0, {root!r})
+import numpy as np
+from stark_amd import engine
+ctx = engine.Context(0)
+fam, C, stop, max_steps, out = {fam!r}, {C}, {stop}, {max_steps}, {out!r}
+if fam == "schools":
+    from oracle import oracle as O
+    m = engine.Model(ctx, "schools", [{{"y": O.SCHOOLS_Y, "sigma": O.SCHOOLS_SIGMA}}])
+else:
+    m = engine.Model.synthetic(ctx, fam, 2, 5000, 8, data_seed=3)
+s = m.sampler(num_warmup=60, num_samples=40, chains=C, seed=11, shard_ids={ids!r})
+s.run(stop, max_steps=max_steps)
+np.save(out, s.save_state())
+print(int(s.iterations().min()), int(s.info()["steps"]))
+"""
+
+
+@pytest.mark.parametrize("fam,C,stop,max_steps", [("logistic", 16, 30, 0), ("logistic", 16, 200, 37),
+                                                  ("linear", 64, 75, 0), ("logistic", 2, 61, 0),
+                                                  ("schools", 8, 30, 0)])
+def test_run_split_across_processes_is_bit_identical(ctx, tmp_path, fam, C, stop, max_steps):
+    """Checkpoint / resume: a run saved by one PROCESS (mid-warmup, mid-trajectory after a step
+    budget, at the warmup/sampling boundary) and loaded into a fresh sampler of another process
+    continues bit for bit as the unsplit run: the same draws, stats, step sizes, metric and
+    gradient counts (stk_sampler_save_state / stk_sampler_load_state)."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    from stark_amd import engine
+    from oracle import oracle as O
+    ids = [5, 2]
+    if fam == "schools":
+        m = engine.Model(ctx, "schools", [{"y": O.SCHOOLS_Y, "sigma": O.SCHOOLS_SIGMA}])
+        ids = [5]
+    else:
+        m = engine.Model.synthetic(ctx, fam, 2, 5000, 8, data_seed=3)
+    cfg = dict(num_warmup=60, num_samples=40, chains=C, seed=11, shard_ids=ids)
+    out = str(tmp_path / "state.npy")
+    r = subprocess.run([sys.executable, "-c", _SAVE_SCRIPT.format(root=ROOT, fam=fam, C=C, stop=stop,
+                                                                   max_steps=max_steps, out=out, ids=ids)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    it_saved, steps_saved = (int(v) for v in r.stdout.split())
+    assert 0 <= it_saved < 100
+    a = m.sampler(**cfg)
+    a.run()
+    b = m.sampler(**cfg)
+    b.load_state(np.load(out))
+    assert int(b.iterations().min()) == it_saved and b.info()["steps"] == steps_saved
+    b.run()
+    for s in range(m.nshards):
+        da, sa = a.draws(s)
+        db, sb = b.draws(s)
+        np.testing.assert_array_equal(da, db)
+        np.testing.assert_array_equal(sa, sb)
+    np.testing.assert_array_equal(a.adaptation()[0], b.adaptation()[0])
+    np.testing.assert_array_equal(a.adaptation()[1], b.adaptation()[1])
+    ia, ib = a.info(), b.info()
+    for k in ("grad_evals", "leapfrogs", "divergent", "steps"):
+        assert ia[k] == ib[k], k
+    # a blob only loads into the run it came from: another seed / chain count is refused
+    c = m.sampler(**{**cfg, "seed": 12})
+    with pytest.raises(engine.StarkHipError, match="another model geometry or sampler config"):
+        c.load_state(np.load(out))
+    c.close()
+    if C != 64:
+        d_ = m.sampler(**{**cfg, "chains": 64 if fam != "schools" else 4})
+        with pytest.raises(engine.StarkHipError):
+            d_.load_state(np.load(out))
+        d_.close()
+    for x in (a, b):
+        x.close()
+    m.close()
+
+
 @pytest.mark.parametrize("C", [4, 16, 64])
 def test_shard_placement_independent(ctx, C):
     """1 GPU holding 4 shards == 4 GPUs holding one shard each (same global shard ids)."""
