@@ -305,7 +305,9 @@ def test_run_split_across_processes_is_bit_identical(ctx, tmp_path, fam, C, stop
     np.testing.assert_array_equal(a.adaptation()[0], b.adaptation()[0])
     np.testing.assert_array_equal(a.adaptation()[1], b.adaptation()[1])
     ia, ib = a.info(), b.info()
-    for k in ("grad_evals", "leapfrogs", "divergent", "steps"):
+    # (not "steps": a run launches steps in batches and may overshoot its last transition by a
+    # few idle ones, so an unsplit run counts a different number of launched steps)
+    for k in ("grad_evals", "leapfrogs", "divergent", "done", "errors"):
         assert ia[k] == ib[k], k
     # a blob only loads into the run it came from: another seed / chain count is refused
     c = m.sampler(**{**cfg, "seed": 12})
