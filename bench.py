@@ -84,10 +84,10 @@ def parse(argv=None):
     p.add_argument("--stepsize-jitter", type=float, default=0.5,
                    help="Stan control stepsize_jitter; breaks the trajectory-length resonance of NUTS on "
                         "this near-isotropic posterior (DESIGN.md section 4)")
-    p.add_argument("--ess-draws", type=int, default=250,
-                   help="post-warmup draws per chain for the ESS / accuracy phase (after the timed steps); "
-                        "ESS/s counts the warmup too, so it rises with the draws per warmup iteration "
-                        "(Stan's defaults: 1000 and 1000)")
+    p.add_argument("--ess-draws", type=int, default=1000,
+                   help="post-warmup draws per chain for the ESS / accuracy phase (after the timed steps): Stan's "
+                        "default num_samples (iter=2000 -> 1000 draws, stark/stark.py:60-63); ESS/s counts the "
+                        "warmup too, so it rises with the draws per warmup iteration (rounds 2-5: 250)")
     p.add_argument("--no-accuracy", action="store_true", help="skip the full-data reference")
     p.add_argument("--nuts-criterion", choices=["stan2.19", "stan2.23"], default="stan2.23",
                    help="stan2.23 (default): Stan's NUTS with the U-turn checks across subtree junctions "
