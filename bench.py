@@ -887,6 +887,8 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # c10d's per-rank rendezvous warnings would fill the stderr the driver keeps beside the line
+    os.environ.setdefault("TORCH_CPP_LOG_LEVEL", "ERROR")
     # STARK_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N-rank path on one
     # GPU (ranks share devices round-robin); the driver's runs use RCCL, one rank per GPU
     backend = os.environ.get("STARK_DIST_BACKEND", "nccl")
