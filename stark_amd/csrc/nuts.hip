@@ -131,43 +131,61 @@ __device__ void mt_init(double* t, int tid, int nthreads) {
     t[i] = v;
   }
 }
-__device__ __forceinline__ double exp_mt(double x, const double* t) {
-  constexpr double MAGIC = 6755399441055744.0;            // 1.5 * 2^52
-  constexpr double INV_L = 184.6649652337873;             // 128 / ln 2
-  constexpr double L_HI = 0.005415212348452769;           // ln2/128 to 32 significant bits
-  constexpr double L_LO = -3.2819649005320973e-13;        // ln2/128 - L_HI
-  const double xc = fmin(fmax(x, -800.0), 800.0);
-  const double sn = fma(xc, INV_L, MAGIC);
+// The fp64 constants of the table math (and the leaf's divergence threshold) as values the
+// compiler cannot see through: it then keeps each in a VGPR pair for the whole launch instead of
+// rematerialising it with two s_mov_b32 at every use (fp64 has no literal operand in VOP3, and at
+// one wave per SIMD every issued instruction costs the wave 4 cycles).  Same values, same
+// operations: bit-identical results.
+struct MtK {
+  double lo, hi, inv_l, magic, l_hi, l_lo, c5, c4, c3, f128, q7, q6, q5, q4, q3, pinf, ninf, div;
+};
+__device__ __forceinline__ double opq(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ MtK mt_consts() {
+  return MtK{opq(-800.0), opq(800.0),
+             opq(184.6649652337873),         // 128 / ln 2
+             opq(6755399441055744.0),        // 1.5 * 2^52
+             opq(0.005415212348452769),      // ln2/128 to 32 significant bits
+             opq(-3.2819649005320973e-13),   // ln2/128 - L_HI
+             opq(1.0 / 120.0), opq(1.0 / 24.0), opq(1.0 / 6.0), opq(128.0),
+             opq(1.0 / 7.0), opq(-1.0 / 6.0), opq(0.2), opq(-0.25), opq(1.0 / 3.0),
+             opq(INFINITY), opq(-INFINITY), opq(1000.0)};
+}
+__device__ __forceinline__ double exp_mt(double x, const double* t, const MtK& k) {
+  const double xc = fmin(fmax(x, k.lo), k.hi);
+  const double sn = fma(xc, k.inv_l, k.magic);
   const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
-  const double n = sn - MAGIC;
-  double r = fma(-n, L_HI, xc);
-  r = fma(-n, L_LO, r);
-  const double p = fma(fma(fma(fma(fma(1.0 / 120.0, r, 1.0 / 24.0), r, 1.0 / 6.0), r, 0.5), r, 1.0), r, 1.0);
+  const double n = sn - k.magic;
+  double r = fma(-n, k.l_hi, xc);
+  r = fma(-n, k.l_lo, r);
+  const double p = fma(fma(fma(fma(fma(k.c5, r, k.c4), r, k.c3), r, 0.5), r, 1.0), r, 1.0);
   const double e = __builtin_amdgcn_ldexp(t[ni & (MT_E - 1)] * p, ni >> 7);
   return x == x ? e : x;
 }
-__device__ __forceinline__ double log1p01_mt(double e, const double* t) {   // e in [0, 1] (NaN kept)
-  const int j = (int)fma(e, 128.0, 0.5);
+__device__ __forceinline__ double log1p01_mt(double e, const double* t, const MtK& k) {   // e in [0, 1] (NaN kept)
+  const int j = (int)fma(e, k.f128, 0.5);
   const double* cj = t + MT_E + 4 * j;
   const dbl2 cd = *reinterpret_cast<const dbl2*>(cj);
   const double rl = fma(e, cd.x, -cd.y);
-  const double q = fma(fma(fma(fma(fma(fma(1.0 / 7.0, rl, -1.0 / 6.0), rl, 0.2), rl, -0.25), rl, 1.0 / 3.0), rl, -0.5), rl, 1.0);
+  const double q = fma(fma(fma(fma(fma(fma(k.q7, rl, k.q6), rl, k.q5), rl, k.q4), rl, k.q3), rl, -0.5), rl, 1.0);
   return fma(rl, q, cj[2]);
 }
 // log_sum_exp_mt that also returns e = exp(-|a - b|), from which the merge's and the top level's
 // acceptance probabilities follow without a second exp (see NutsChain::on_leaf)
-__device__ __forceinline__ double log_sum_exp_mt_e(double a, double b, const double* t, double& e) {
-  e = exp_mt(-fabs(a - b), t);
-  const double r = fmax(a, b) + log1p01_mt(e, t);
-  const double r1 = (a == INFINITY && b == INFINITY) ? INFINITY : r;
-  return a == -INFINITY ? b : r1;
+__device__ __forceinline__ double log_sum_exp_mt_e(double a, double b, const double* t, const MtK& k, double& e) {
+  e = exp_mt(-fabs(a - b), t, k);
+  const double r = fmax(a, b) + log1p01_mt(e, t, k);
+  const double r1 = (a == k.pinf && b == k.pinf) ? k.pinf : r;
+  return a == k.ninf ? b : r1;
 }
-__device__ __forceinline__ double log_sum_exp_mt(double a, double b, const double* t) {   // as log_sum_exp2
+__device__ __forceinline__ double log_sum_exp_mt(double a, double b, const double* t, const MtK& k) {   // as log_sum_exp2
   // branch-free: max + log1p(exp(-|a - b|)), with log_sum_exp2's two special cases as selects
   // (a = -inf with b finite needs none: exp(-inf) = 0 gives b)
-  const double r = fmax(a, b) + log1p01_mt(exp_mt(-fabs(a - b), t), t);
-  const double r1 = (a == INFINITY && b == INFINITY) ? INFINITY : r;
-  return a == -INFINITY ? b : r1;
+  const double r = fmax(a, b) + log1p01_mt(exp_mt(-fabs(a - b), t, k), t, k);
+  const double r1 = (a == k.pinf && b == k.pinf) ? k.pinf : r;
+  return a == k.ninf ? b : r1;
 }
 
 // ------------------------------------------------------------------ model hooks
@@ -190,11 +208,12 @@ __device__ __forceinline__ void schools_data(const ShardDev& sh, double (&yc)[NC
 }
 template <int NCH, int SEG = WAVE, bool FM = false>
 __device__ double schools_lpgrad(const double (&yc)[NCH], const double (&isc)[NCH], const double (&q)[NCH],
-                                 double (&glp)[NCH], int lane, int D, const double* mt = nullptr) {
+                                 double (&glp)[NCH], int lane, int D, const double* mt = nullptr,
+                                 const MtK* mk = nullptr) {
   const double mu = seg_bcast<SEG, 0>(q[0]);
   const double u = seg_bcast<SEG, 1>(q[0]);
   double tau;
-  if constexpr (FM) tau = exp_mt(u, mt);
+  if constexpr (FM) tau = exp_mt(u, mt, *mk);
   else tau = exp(u);
   double lp = 0.0, smu = 0.0, su = 0.0;
 #pragma unroll
@@ -299,12 +318,13 @@ struct NutsChain {
   int iv[I_COUNT];
   double q[NCH], p[NCH], g[NCH], im[NCH];
   const double* mt = nullptr;     // FM: the fused kernel's exp / log1p table in LDS (else ocml)
+  MtK mk{};                       // FM: its constants, VGPR-resident (mt_consts)
   __device__ __forceinline__ double ex(double x) const {
-    if constexpr (FM) return exp_mt(x, mt);
+    if constexpr (FM) return exp_mt(x, mt, mk);
     else return exp(x);
   }
   __device__ __forceinline__ double lse(double a, double b) const {
-    if constexpr (FM) return log_sum_exp_mt(a, b, mt);
+    if constexpr (FM) return log_sum_exp_mt(a, b, mt, mk);
     else return log_sum_exp2(a, b);
   }
   uint32_t nleap = 0, ndiv = 0;   // leapfrogs / divergent draws since the last flush_counts()
@@ -714,8 +734,13 @@ struct NutsChain {
     ++nleap;
     const double H0 = S(S_H0);
     double h = S(S_V) + kinetic(p);
-    if (isnan(h)) h = INFINITY;
-    if ((h - H0) > 1000.0) IV(I_DIV) = 1;
+    if constexpr (FM) {
+      if (isnan(h)) h = mk.pinf;
+      if ((h - H0) > mk.div) IV(I_DIV) = 1;
+    } else {
+      if (isnan(h)) h = INFINITY;
+      if ((h - H0) > 1000.0) IV(I_DIV) = 1;
+    }
     IV(I_NLEAP) += 1;
     S(S_SUMMETRO) += (H0 - h > 0) ? 1.0 : ex(H0 - h);
     // the leaf as a depth-0 sub-tree
@@ -753,7 +778,7 @@ struct NutsChain {
         // the log_sum_exp, u < 1/(1 + e) (c >= l) or e/(1 + e) (c < l), compared without a division
         // (c_lsw > lsw_sub never holds); the same decision up to the last bits of the probability
         double e;
-        lsw_sub = log_sum_exp_mt_e(l_lsw, c_lsw, mt, e);
+        lsw_sub = log_sum_exp_mt_e(l_lsw, c_lsw, mt, mk, e);
         take_right = u * (1.0 + e) < (c_lsw >= l_lsw ? 1.0 : e);
       } else {
         lsw_sub = lse(l_lsw, c_lsw);
@@ -843,7 +868,7 @@ struct NutsChain {
       double lsw_new;
       if constexpr (FM) {   // one exp for both: e = exp(-|c_lsw - lsw|) is exp(c_lsw - lsw) when c_lsw <= lsw
         double e;
-        lsw_new = log_sum_exp_mt_e(S(S_LSW), c_lsw, mt, e);
+        lsw_new = log_sum_exp_mt_e(S(S_LSW), c_lsw, mt, mk, e);
         take = c_lsw > S(S_LSW) || u < e;
       } else {
         take = c_lsw > S(S_LSW) || u < ex(c_lsw - S(S_LSW));
@@ -1056,6 +1081,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   if (run) {
     NutsChain<NCH, SEG, true, UT> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
     ch.mt = mtab;
+    ch.mk = mt_consts();
     ch.ub = fl + ((nv + ns + nss + nsc + 1) & ~(size_t)1);   // after the chain's image, 16-B aligned: 2 SEG doubles
     ch.load();
     ch.fill_uniforms(ch.IV(I_UK) & ~1);                // the current transition's window (a resumed chain)
@@ -1080,7 +1106,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
       while (req && steps < max_steps) {
         double glp[NCH];
         ch.ensure_uniforms();
-        const double lp = schools_lpgrad<NCH, SEG, true>(yc, isc, ch.q, glp, lane, ch.D, mtab);
+        const double lp = schools_lpgrad<NCH, SEG, true>(yc, isc, ch.q, glp, lane, ch.D, mtab, &ch.mk);
         ++steps;
         req = ch.consume(lp, glp, pause_at);
         if (req) ++ngrad;
