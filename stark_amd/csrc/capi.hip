@@ -688,6 +688,9 @@ int stk_sampler_create(stk_model* m, const stk_config* cfg, stk_sampler** out) {
   if (rc == STK_OK) {
     hipError_t e = stk_launch_nuts_init(A, init_dev, im_dev, cfg->stepsize, cfg->init_radius, ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(A.draws, 0, sizeof(double) * (size_t)m->nshards * m->Pmax * A.S_total, ctx->stream);
+    // a zeroed tree stack: the fused kernel's zero-padding form relies on +0 in every padding slot
+    if (e == hipSuccess)
+      e = hipMemsetAsync(A.stk, 0, sizeof(double) * (size_t)nchains * cfg->max_depth * SV_COUNT * Dp, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) {
       stk_set_error("sampler init: %s", hipGetErrorString(e));

@@ -295,7 +295,7 @@ __device__ __forceinline__ void write_draw(const NutsArgs& A, const ShardDev& sh
 // ------------------------------------------------------------------ the chain
 // SEG: lanes per chain (64: one chain per wave; 16 / 32: 4 / 2 chains packed in a wave, each
 // in its own DPP row(s), D <= SEG).  `lane` is the lane's position inside its segment.
-template <int NCH, int SEG = WAVE, bool FM = false, int UT = -1>
+template <int NCH, int SEG = WAVE, bool FM = false, int UT = -1, bool ZP = false>
 // UT: the U-turn criterion at compile time (0: Stan 2.19, 1: Stan >= 2.23's junction checks; -1: at
 // run time from A.uturn_ext) -- a run-time branch on it splits the merge loop's basic block
 // (every member is force-inlined: a non-inlined constructor or method receiving `this` puts
@@ -364,6 +364,16 @@ struct NutsChain {
     else return A.uturn_ext != 0;
   }
   __device__ __forceinline__ bool ok(int k) const { return k * SEG + lane < D; }
+  // ZP (the fused kernel when every lane of a chain's segment reads inside its own vector,
+  // Dp >= SEG NCH): the lanes past D hold +0 in every vector register and in every padding slot of
+  // the LDS image -- momenta are drawn as 0 there, the gradient is 0 there, and q, p, rho, p_sharp,
+  // the Welford sums follow from them; the tree stack starts zeroed (stk_sampler_create) -- so the
+  // LDS reads need no select, the stores no exec mask and the dot products no masked adds: the
+  // padding lanes contribute exact zeros.  Vector arithmetic then uses okv() instead of ok().
+  __device__ __forceinline__ bool okv(int k) const {
+    if constexpr (FM && ZP) return true;
+    else return ok(k);
+  }
   __device__ __forceinline__ double* vp(int v) const { return vec + (size_t)v * A.Dp; }
   __device__ __forceinline__ double* svp(int level, int v) const {
     return stk + ((size_t)level * (uext() ? SV_COUNT : SV_PB) + v) * A.Dp;   // stack_vecs(A)
@@ -377,7 +387,7 @@ struct NutsChain {
     for (int k = 0; k < NCH; ++k) {
       if constexpr (FM) {
         const double v = base[k * SEG + lane];
-        r[k] = ok(k) ? v : 0.0;
+        r[k] = okv(k) ? v : 0.0;
       } else {
         r[k] = ok(k) ? base[k * SEG + lane] : 0.0;
       }
@@ -390,7 +400,7 @@ struct NutsChain {
   __device__ __forceinline__ void st(double* base, const double (&r)[NCH]) const {
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
-      if (ok(k)) base[k * SEG + lane] = r[k];
+      if (okv(k)) base[k * SEG + lane] = r[k];
   }
 
   __device__ __forceinline__ void load() {
@@ -438,14 +448,14 @@ struct NutsChain {
     double t = 0.0;
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
-      if (ok(k)) t += pp[k] * im[k] * pp[k];
+      if (okv(k)) t += pp[k] * im[k] * pp[k];
     return 0.5 * seg_sum<SEG>(t);
   }
   __device__ __forceinline__ bool criterion(const double (&psm)[NCH], const double (&psp)[NCH], const double (&rho)[NCH]) const {
     double a = 0.0, b = 0.0;
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
-      if (ok(k)) { a += psp[k] * rho[k]; b += psm[k] * rho[k]; }
+      if (okv(k)) { a += psp[k] * rho[k]; b += psm[k] * rho[k]; }
     a = seg_sum<SEG>(a);
     b = seg_sum<SEG>(b);
     return a > 0 && b > 0;
@@ -1045,7 +1055,7 @@ __global__ __launch_bounds__(64) void k_nuts_step(NutsArgs A, int step_id, int p
 // chain per wave leaves 54 of 64 lanes idle, four per wave leave 24.  Every chain still runs
 // its own state machine; lanes of one chain always take the same branch, and the segmented
 // sums stay inside a chain's DPP row(s), so chains in other states never interfere.
-template <int NCH, int CPW, int MINW = 1, int UT = 0>
+template <int NCH, int CPW, int MINW = 1, int UT = 0, bool ZP = false>
 __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int pause_at, int max_steps) {
   constexpr int SEG = WAVE / CPW;
   static_assert(CPW == 1 || NCH == 1, "packed chains hold one chunk of lanes each");
@@ -1079,7 +1089,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   }
   __syncthreads();
   if (run) {
-    NutsChain<NCH, SEG, true, UT> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
+    NutsChain<NCH, SEG, true, UT, ZP> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
     ch.mt = mtab;
     ch.mk = mt_consts();
     ch.ub = fl + ((nv + ns + nss + nsc + 1) & ~(size_t)1);   // after the chain's image, 16-B aligned: 2 SEG doubles
@@ -1164,8 +1174,8 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
   hipLaunchKernelGGL(k_nuts_step<NCH>, dim3(A.nchains), dim3(64), 0, st, A, step_id, pause_at);
   return hipGetLastError();
 }
-template <int NCH, int CPW, int MINW = 1, int UT = 0>
-static hipError_t launch_fused_ut(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
+template <int NCH, int CPW, int MINW = 1, int UT = 0, bool ZP = false>
+static hipError_t launch_fused_zp(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
   constexpr int SEG = WAVE / CPW;
   size_t per = (size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp + (size_t)A.max_depth * SS_COUNT +
                S_COUNT + (I_COUNT + 1) / 2 + 2 * SEG;  // + the chain's uniform window
@@ -1174,11 +1184,20 @@ static hipError_t launch_fused_ut(const NutsArgs& A, int pause_at, int max_steps
   if (lds > 64 * 1024) {
     // the attribute is per device (allow_big_lds keys it on the current one); a failure is
     // reported as such rather than as a generic launch failure
-    if (const hipError_t e = allow_big_lds((const void*)k_nuts_fused_schools<NCH, CPW, MINW, UT>)) return e;
+    if (const hipError_t e = allow_big_lds((const void*)k_nuts_fused_schools<NCH, CPW, MINW, UT, ZP>)) return e;
   }
-  hipLaunchKernelGGL((k_nuts_fused_schools<NCH, CPW, MINW, UT>), dim3((A.nchains + CPW - 1) / CPW), dim3(64), lds, st,
-                     A, pause_at, max_steps);
+  hipLaunchKernelGGL((k_nuts_fused_schools<NCH, CPW, MINW, UT, ZP>), dim3((A.nchains + CPW - 1) / CPW), dim3(64), lds,
+                     st, A, pause_at, max_steps);
   return hipGetLastError();
+}
+// the zero-padding form (NutsChain ZP) where a chain's segment lies inside its vectors: 4 chains
+// per wave at Dp = 16 (8 schools, J = 8..14)
+template <int NCH, int CPW, int MINW = 1, int UT = 0>
+static hipError_t launch_fused_ut(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
+  if constexpr (CPW == 4 && NCH == 1) {
+    if (A.Dp >= WAVE / CPW) return launch_fused_zp<NCH, CPW, MINW, UT, true>(A, pause_at, max_steps, st);
+  }
+  return launch_fused_zp<NCH, CPW, MINW, UT, false>(A, pause_at, max_steps, st);
 }
 template <int NCH, int CPW, int MINW = 1>
 static hipError_t launch_fused_t(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
