@@ -364,8 +364,7 @@ struct NutsChain {
     else return A.uturn_ext != 0;
   }
   __device__ __forceinline__ bool ok(int k) const { return k * SEG + lane < D; }
-  // ZP (the fused kernel when every lane of a chain's segment reads inside its own vector,
-  // Dp >= SEG NCH): the lanes past D hold +0 in every vector register and in every padding slot of
+  // ZP (the fused kernel when a chain's segment spans exactly its vectors, Dp = SEG NCH): the lanes past D hold +0 in every vector register and in every padding slot of
   // the LDS image -- momenta are drawn as 0 there, the gradient is 0 there, and q, p, rho, p_sharp,
   // the Welford sums follow from them; the tree stack starts zeroed (stk_sampler_create) -- so the
   // LDS reads need no select, the stores no exec mask and the dot products no masked adds: the
@@ -374,9 +373,15 @@ struct NutsChain {
     if constexpr (FM && ZP) return true;
     else return ok(k);
   }
-  __device__ __forceinline__ double* vp(int v) const { return vec + (size_t)v * A.Dp; }
+  // the vector stride: ZP runs only at Dp = SEG NCH, a compile-time constant, so every vector of
+  // the LDS image sits at an immediate offset from one base (no per-vector address registers)
+  __device__ __forceinline__ int dp() const {
+    if constexpr (FM && ZP) return SEG * NCH;
+    else return A.Dp;
+  }
+  __device__ __forceinline__ double* vp(int v) const { return vec + (size_t)v * dp(); }
   __device__ __forceinline__ double* svp(int level, int v) const {
-    return stk + ((size_t)level * (uext() ? SV_COUNT : SV_PB) + v) * A.Dp;   // stack_vecs(A)
+    return stk + ((size_t)level * (uext() ? SV_COUNT : SV_PB) + v) * dp();   // stack_vecs(A)
   }
   // FM (the fused kernel, where every vector lives in the workgroup's LDS image): the load is
   // unconditional and lanes past D select 0 -- an exec-masked load would split the basic block
@@ -1063,7 +1068,8 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   const int gid = blockIdx.x * CPW + seg;
   const bool live = gid < A.nchains;
   extern __shared__ double fl_all[];
-  const size_t nv = (size_t)V_COUNT * A.Dp, ns = (size_t)A.max_depth * stack_vecs(A) * A.Dp;
+  const int dpk = ZP ? SEG * NCH : A.Dp;                 // ZP: Dp = SEG NCH at compile time
+  const size_t nv = (size_t)V_COUNT * dpk, ns = (size_t)A.max_depth * stack_vecs(A) * dpk;
   const size_t nss = (size_t)A.max_depth * SS_COUNT;
   constexpr size_t nsc = S_COUNT + (I_COUNT + 1) / 2;   // the chain's scalars and counters
   const size_t per = (nv + ns + nss + nsc + 2 * SEG + 1) & ~(size_t)1;   // per-chain image + uniform window, even
@@ -1195,7 +1201,7 @@ static hipError_t launch_fused_zp(const NutsArgs& A, int pause_at, int max_steps
 template <int NCH, int CPW, int MINW = 1, int UT = 0>
 static hipError_t launch_fused_ut(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
   if constexpr (CPW == 4 && NCH == 1) {
-    if (A.Dp >= WAVE / CPW) return launch_fused_zp<NCH, CPW, MINW, UT, true>(A, pause_at, max_steps, st);
+    if (A.Dp == WAVE / CPW) return launch_fused_zp<NCH, CPW, MINW, UT, true>(A, pause_at, max_steps, st);
   }
   return launch_fused_zp<NCH, CPW, MINW, UT, false>(A, pause_at, max_steps, st);
 }

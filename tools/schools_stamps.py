@@ -52,9 +52,9 @@ def instrument(s):
     assert leaf.count("stamp()") == 8, leaf.count("stamp()")
     s = s[:body_start] + leaf + s[body_end:]
     # the fused loop
-    sub("        const double lp = schools_lpgrad<NCH, SEG, true>(yc, isc, ch.q, glp, lane, ch.D, mtab);\n        ++steps;\n        req = ch.consume(lp, glp, pause_at);",
+    sub("        const double lp = schools_lpgrad<NCH, SEG, true>(yc, isc, ch.q, glp, lane, ch.D, mtab, &ch.mk);\n        ++steps;\n        req = ch.consume(lp, glp, pause_at);",
         "        const unsigned long long t0 = stamp();\n"
-        "        const double lp = schools_lpgrad<NCH, SEG, true>(yc, isc, ch.q, glp, lane, ch.D, mtab);\n"
+        "        const double lp = schools_lpgrad<NCH, SEG, true>(yc, isc, ch.q, glp, lane, ch.D, mtab, &ch.mk);\n"
         "        const unsigned long long t1 = stamp();\n        ++steps;\n        req = ch.consume(lp, glp, pause_at);\n"
         "        ch.stp[0] += t1 - t0;\n        ch.stp[1] += stamp() - t1;\n        ch.stp[7] += 1;")
     sub("      ch.save();\n      ch.flush_counts();\n      if (req) ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);",
