@@ -180,6 +180,25 @@ __device__ __forceinline__ double log_sum_exp_mt_e(double a, double b, const dou
   const double r1 = (a == k.pinf && b == k.pinf) ? k.pinf : r;
   return a == k.ninf ? b : r1;
 }
+// The tree's own log_sum_exp (the merge of two sub-trees' log weights, and of the trajectory's
+// with a new sub-tree's): both weights are finite there -- a divergent leaf (energy error > 1000
+// or NaN) stops the transition before any merge -- so log_sum_exp2's two infinite cases cannot
+// occur and their selects go; exp's argument -|a - b| is <= 0, so only the lower clamp stays;
+// NaN still propagates (a NaN weight gives a NaN sum, as before).  At one wave per SIMD every
+// issued instruction costs the wave 4 cycles, and this runs once per merge.
+__device__ __forceinline__ double log_sum_exp_mt_e_tree(double a, double b, const double* t, const MtK& k, double& e) {
+  const double x = -fabs(a - b);
+  const double xc = fmax(x, k.lo);
+  const double sn = fma(xc, k.inv_l, k.magic);
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, sn);
+  const double n = sn - k.magic;
+  double r = fma(-n, k.l_hi, xc);
+  r = fma(-n, k.l_lo, r);
+  const double p = fma(fma(fma(fma(fma(k.c5, r, k.c4), r, k.c3), r, 0.5), r, 1.0), r, 1.0);
+  const double ee = __builtin_amdgcn_ldexp(t[ni & (MT_E - 1)] * p, ni >> 7);
+  e = x == x ? ee : x;
+  return fmax(a, b) + log1p01_mt(e, t, k);
+}
 __device__ __forceinline__ double log_sum_exp_mt(double a, double b, const double* t, const MtK& k) {   // as log_sum_exp2
   // branch-free: max + log1p(exp(-|a - b|)), with log_sum_exp2's two special cases as selects
   // (a = -inf with b finite needs none: exp(-inf) = 0 gives b)
@@ -793,7 +812,7 @@ struct NutsChain {
         // the log_sum_exp, u < 1/(1 + e) (c >= l) or e/(1 + e) (c < l), compared without a division
         // (c_lsw > lsw_sub never holds); the same decision up to the last bits of the probability
         double e;
-        lsw_sub = log_sum_exp_mt_e(l_lsw, c_lsw, mt, mk, e);
+        lsw_sub = log_sum_exp_mt_e_tree(l_lsw, c_lsw, mt, mk, e);
         take_right = u * (1.0 + e) < (c_lsw >= l_lsw ? 1.0 : e);
       } else {
         lsw_sub = lse(l_lsw, c_lsw);
@@ -883,7 +902,7 @@ struct NutsChain {
       double lsw_new;
       if constexpr (FM) {   // one exp for both: e = exp(-|c_lsw - lsw|) is exp(c_lsw - lsw) when c_lsw <= lsw
         double e;
-        lsw_new = log_sum_exp_mt_e(S(S_LSW), c_lsw, mt, mk, e);
+        lsw_new = log_sum_exp_mt_e_tree(S(S_LSW), c_lsw, mt, mk, e);
         take = c_lsw > S(S_LSW) || u < e;
       } else {
         take = c_lsw > S(S_LSW) || u < ex(c_lsw - S(S_LSW));
@@ -989,6 +1008,7 @@ struct NutsChain {
 };
 
 // ------------------------------------------------------------------ kernels
+#ifndef STK_NUTS_FUSED4_TU
 __global__ __launch_bounds__(64) void k_nuts_init(NutsArgs A, const double* init, const double* inv_metric,
                                                   double stepsize, double init_radius) {
   const int gid = blockIdx.x, lane = threadIdx.x;
@@ -1028,6 +1048,7 @@ __global__ __launch_bounds__(64) void k_nuts_init(NutsArgs A, const double* init
   }
 }
 
+#endif  // STK_NUTS_FUSED4_TU
 template <int NCH>
 __global__ __launch_bounds__(64) void k_nuts_step(NutsArgs A, int step_id, int pause_at) {
   const int gid = blockIdx.x, lane = threadIdx.x;
@@ -1196,12 +1217,22 @@ static hipError_t launch_fused_zp(const NutsArgs& A, int pause_at, int max_steps
                      st, A, pause_at, max_steps);
   return hipGetLastError();
 }
-// the zero-padding form (NutsChain ZP) where a chain's segment lies inside its vectors: 4 chains
-// per wave at Dp = 16 (8 schools, J = 8..14)
+// The zero-padding form (NutsChain ZP) where a chain's segment spans its vectors: 4 chains per wave
+// at Dp = 16 (8 schools, J = 8..14).  It is instantiated in its own translation unit,
+// nuts_fused4.hip (this file with STK_NUTS_FUSED4_TU), so that it alone is built with LLVM's
+// iterative ILP scheduler (Makefile): that experimental scheduler gains it 2-3 % but has crashed
+// the compiler on other instantiations of this file.
+hipError_t stk_launch_fused4_zp(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st);
+#ifdef STK_NUTS_FUSED4_TU
+hipError_t stk_launch_fused4_zp(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
+  return A.uturn_ext ? launch_fused_zp<1, 4, 1, 1, true>(A, pause_at, max_steps, st)
+                     : launch_fused_zp<1, 4, 1, 0, true>(A, pause_at, max_steps, st);
+}
+#else
 template <int NCH, int CPW, int MINW = 1, int UT = 0>
 static hipError_t launch_fused_ut(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
   if constexpr (CPW == 4 && NCH == 1) {
-    if (A.Dp == WAVE / CPW) return launch_fused_zp<NCH, CPW, MINW, UT, true>(A, pause_at, max_steps, st);
+    if (A.Dp == WAVE / CPW) return stk_launch_fused4_zp(A, pause_at, max_steps, st);
   }
   return launch_fused_zp<NCH, CPW, MINW, UT, false>(A, pause_at, max_steps, st);
 }
@@ -1265,3 +1296,4 @@ hipError_t stk_launch_schools_lpgrad(const ShardDev* shards, int shard, int nch,
     return hipErrorInvalidValue;
   return hipGetLastError();
 }
+#endif  // STK_NUTS_FUSED4_TU

@@ -10,7 +10,8 @@ each workload reports whether the arms' results are bit-identical.
                        chains): k_sweep16's ms per launch (HIP events), identical = grads agree
              fulldata  tools/bench_fulldata.py --steps 6 (configs[4] at 1e7 rows): pass F + B ms
 
-usage: tools/lib_ab.py build NAME [--rev REV] [--flags FILE=FLAGS ...]   (here; -> tools/_bin/ab_NAME)
+usage: tools/lib_ab.py build NAME [--rev REV] [--flags FILE=FLAGS ...]   (here; -> tools/_bin/ab_NAME; no
+       --flags: the tree's Makefile)
        tools/lib_ab.py run --arms A,B[,C] --work schools|sweep16|fulldata [--rounds R]   (GPU box)"""
 import argparse
 import json
@@ -20,7 +21,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "tools", "_bin")
-SRCS = ["capi.hip", "nuts.hip", "sweep.hip", "sweep16.hip", "datagen.hip", "combine.hip"]
+SRCS = ["capi.hip", "nuts.hip", "nuts_fused4.hip", "sweep.hip", "sweep16.hip", "datagen.hip", "combine.hip"]
 BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fvisibility=hidden"]
 
 
@@ -40,6 +41,11 @@ def build(name, rev=None, flags=()):
     for f in flags:
         k, v = f.split("=", 1)
         extra[k] = v.split()
+    if not extra:        # the tree's own Makefile (its per-file flags)
+        subprocess.run(["make", "-s", "-j8", "-C", csrc, f"OUT={out}"], check=True)
+        json.dump({"rev": rev or "working tree", "flags": "Makefile"}, open(os.path.join(out, "arm.json"), "w"))
+        print("built", os.path.join(out, "libstark_hip.so"), "with the Makefile")
+        return
     procs, objs = [], []
     for s in SRCS:
         o = os.path.join(out, s.replace(".hip", ".o"))
@@ -70,7 +76,7 @@ def one(arm, work):
     if work == "schools":
         return ln["value"] / 1e6, [ln[k] for k in ("posterior_mean_mu_tau", "min_ess", "divergent", "leapfrogs_per_transition")]
     if work == "sweep16":
-        return ln["roofline"]["avg_launch_ms"], [ln["value"] * ln["ms_per_step"]]
+        return ln["roofline"]["avg_launch_ms"], [round(ln["value"] * ln["ms_per_step"])]
     return ln["roofline"]["avg_launch_ms"], [ln.get("chains_sha16_per_rank")]
 
 
