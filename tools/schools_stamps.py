@@ -61,8 +61,10 @@ def instrument(s):
         "      ch.save();\n      ch.flush_counts();\n      if (lane == 0 && gid < 8192)\n"
         "        for (int i = 0; i < 8; ++i) stk_stamp_acc[(size_t)gid * 8 + i] += ch.stp[i];\n"
         "      if (req) ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);")
-    s += ("\nextern \"C\" __attribute__((visibility(\"default\"))) int stk_debug_stamps(unsigned long long* out, int n) {\n"
-          "  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(stk::stk_stamp_acc), sizeof(unsigned long long) * n);\n}\n")
+    # nuts.hip is compiled twice (nuts.o, and nuts_fused4.o for the 4-chains-per-wave kernel):
+    # the export lives in the second, whose accumulators the 8-schools run fills
+    s += ("\n#ifdef STK_NUTS_FUSED4_TU\nextern \"C\" __attribute__((visibility(\"default\"))) int stk_debug_stamps(unsigned long long* out, int n) {\n"
+          "  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(stk::stk_stamp_acc), sizeof(unsigned long long) * n);\n}\n#endif\n")
     return s
 
 
