@@ -426,6 +426,67 @@ struct NutsChain {
     for (int k = 0; k < NCH; ++k)
       if (okv(k)) base[k * SEG + lane] = r[k];
   }
+  // The trajectory's vectors (z+, z-, the sample point, rho, p_sharp, the metric and its Welford
+  // sums): RV (the fused kernel in its zero-padding form) keeps them in registers for the whole
+  // launch -- at one wave per SIMD nothing hides an LDS round trip, and the register file has room
+  // (the tree stack, indexed by level at run time, stays in LDS).  Otherwise they live at vp(v).
+  // Every vector index below is a compile-time constant after inlining (a run-time index into rv
+  // would put it in scratch); the two-way choices go through vld_sel / vst_sel.
+  static constexpr bool RV = FM && ZP;
+  double rv[RV ? V_COUNT : 1][NCH];
+  __device__ __forceinline__ void vld(int v, double (&r)[NCH]) const {
+    if constexpr (RV) {
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) r[k] = rv[v][k];
+    } else {
+      ld(vp(v), r);
+    }
+  }
+  __device__ __forceinline__ void vst(int v, const double (&r)[NCH]) {
+    if constexpr (RV) {
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) rv[v][k] = r[k];
+    } else {
+      st(vp(v), r);
+    }
+  }
+  __device__ __forceinline__ void vld_sel(bool c, int va, int vb, double (&r)[NCH]) const {   // c ? va : vb
+    if constexpr (RV) {
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) r[k] = c ? rv[va][k] : rv[vb][k];
+    } else {
+      ld(vp(c ? va : vb), r);
+    }
+  }
+  __device__ __forceinline__ void vst_sel(bool c, int va, int vb, const double (&r)[NCH]) {   // into c ? va : vb
+    if constexpr (RV) {
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        rv[va][k] = c ? r[k] : rv[va][k];
+        rv[vb][k] = c ? rv[vb][k] : r[k];
+      }
+    } else {
+      st(vp(c ? va : vb), r);
+    }
+  }
+  // RV: the launch's copy of the vectors in and out of the chain's global block (Dp = SEG NCH: every
+  // lane of every vector, padding zeros included)
+  __device__ __forceinline__ void rv_in(const double* gvec) {
+    if constexpr (RV) {
+#pragma unroll
+      for (int v = 0; v < V_COUNT; ++v)
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) rv[v][k] = gvec[(size_t)v * dp() + k * SEG + lane];
+    }
+  }
+  __device__ __forceinline__ void rv_out(double* gvec) const {
+    if constexpr (RV) {
+#pragma unroll
+      for (int v = 0; v < V_COUNT; ++v)
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) gvec[(size_t)v * dp() + k * SEG + lane] = rv[v][k];
+    }
+  }
 
   __device__ __forceinline__ void load() {
     load_scalars();
@@ -442,10 +503,10 @@ struct NutsChain {
       if (!cold_i(i)) iv[i] = ivp[i];
   }
   __device__ __forceinline__ void load_vectors() {
-    ld(vp(V_Q), q);
-    ld(vp(V_P), p);
-    ld(vp(V_G), g);
-    ld(vp(V_IM), im);
+    vld(V_Q, q);
+    vld(V_P, p);
+    vld(V_G, g);
+    vld(V_IM, im);
   }
   __device__ __forceinline__ void flush_counts() {
     if (lane == 0 && (nleap | ndiv)) {
@@ -454,7 +515,7 @@ struct NutsChain {
     }
     nleap = ndiv = 0;
   }
-  __device__ __forceinline__ void save() const {
+  __device__ __forceinline__ void save() {
     double* sc = A.sc + (size_t)gid * S_COUNT;
     int* ivp = A.iv + (size_t)gid * I_COUNT;
 #pragma unroll
@@ -463,9 +524,9 @@ struct NutsChain {
 #pragma unroll
     for (int i = 0; i < I_COUNT; ++i)
       if (!cold_i(i)) ivp[i] = iv[i];
-    st(vp(V_Q), q);
-    st(vp(V_P), p);
-    st(vp(V_G), g);
+    vst(V_Q, q);
+    vst(V_P, p);
+    vst(V_G, g);
   }
 
   __device__ __forceinline__ double kinetic(const double (&pp)[NCH]) const {   // diag_e_metric::tau
@@ -531,8 +592,8 @@ struct NutsChain {
     }
   }
   __device__ __forceinline__ void load_sample_point() {
-    ld(vp(V_QS), q);
-    ld(vp(V_GS), g);
+    vld(V_QS, q);
+    vld(V_GS, g);
     S(S_V) = S(S_VS);
   }
 
@@ -583,11 +644,11 @@ struct NutsChain {
     const unsigned nw = (unsigned)A.num_warmup;
     const bool in_window = (cnt >= A.init_buffer) && (cnt < nw - A.term_buffer) && (cnt != nw);
     double wm[NCH], wm2[NCH];
-    ld(vp(V_WM), wm);
-    ld(vp(V_WM2), wm2);
+    vld(V_WM, wm);
+    vld(V_WM2, wm2);
     if (in_window) {
       double qs[NCH];
-      ld(vp(V_QS), qs);
+      vld(V_QS, qs);
       S(S_WFN) += 1.0;
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
@@ -620,10 +681,10 @@ struct NutsChain {
         wm2[k] = 0.0;
       }
       S(S_WFN) = 0.0;
-      st(vp(V_IM), im);
+      vst(V_IM, im);
     }
-    st(vp(V_WM), wm);
-    st(vp(V_WM2), wm2);
+    vst(V_WM, wm);
+    vst(V_WM2, wm2);
     IV(I_WCNT) = (int)(cnt + 1);
     return end_window;
   }
@@ -632,9 +693,9 @@ struct NutsChain {
   __device__ __forceinline__ void begin_subtree() {
     IV(I_DIR) = uniform() > 0.5 ? 1 : -1;
     const int f = IV(I_DIR) > 0;
-    ld(vp(f ? V_QF : V_QB), q);
-    ld(vp(f ? V_PF : V_PB), p);
-    ld(vp(f ? V_GF : V_GB), g);
+    vld_sel(f, V_QF, V_QB, q);
+    vld_sel(f, V_PF, V_PB, p);
+    vld_sel(f, V_GF, V_GB, g);
     S(S_V) = f ? S(S_VF) : S(S_VB);
     IV(I_LEAF) = 0;
     begin_leapfrog(IV(I_DIR) * S(S_EPS));
@@ -652,16 +713,16 @@ struct NutsChain {
     const double H0 = S(S_V) + kinetic(p);
     S(S_H0) = H0;
     S(S_HS) = H0;
-    st(vp(V_QF), q); st(vp(V_PF), p); st(vp(V_GF), g);
-    st(vp(V_QB), q); st(vp(V_PB), p); st(vp(V_GB), g);
+    vst(V_QF, q); vst(V_PF, p); vst(V_GF, g);
+    vst(V_QB, q); vst(V_PB, p); vst(V_GB, g);
     S(S_VF) = S(S_V);
     S(S_VB) = S(S_V);
     double ps[NCH];
 #pragma unroll
     for (int k = 0; k < NCH; ++k) ps[k] = im[k] * p[k];
-    st(vp(V_PSP), ps);
-    st(vp(V_PSM), ps);
-    st(vp(V_RHO), p);
+    vst(V_PSP, ps);
+    vst(V_PSM, ps);
+    vst(V_RHO, p);
     S(S_LSW) = 0.0;
     S(S_SUMMETRO) = 0.0;
     IV(I_NLEAP) = 0;
@@ -684,13 +745,13 @@ struct NutsChain {
     const int it = IV(I_ITER);
     if (it >= A.ud_first) {
       double qs[NCH];
-      ld(vp(V_QS), qs);
+      vld(V_QS, qs);
       st(A.udraws + ((size_t)gid * A.ud_iters + (it - A.ud_first)) * A.Dp, qs);
     }
     if (it >= A.num_warmup) {
       const int col = cidx * A.num_samples + (it - A.num_warmup);
       double qs[NCH];
-      ld(vp(V_QS), qs);
+      vld(V_QS, qs);
       write_draw<NCH, SEG>(A, sh, shard, col, qs, -S(S_VS), lane);
       if (lane < N_STATS) {
         double v = 0;
@@ -887,12 +948,12 @@ struct NutsChain {
       const int fwd = IV(I_DIR) > 0;
       double o_p[NCH], o_ps[NCH];     // the old trajectory's end next to the new sub-tree
       if (uext()) {
-        ld(vp(fwd ? V_PF : V_PB), o_p);
-        ld(vp(fwd ? V_PSP : V_PSM), o_ps);
+        vld_sel(fwd, V_PF, V_PB, o_p);
+        vld_sel(fwd, V_PSP, V_PSM, o_ps);
       }
-      st(vp(fwd ? V_QF : V_QB), q);
-      st(vp(fwd ? V_PF : V_PB), p);
-      st(vp(fwd ? V_GF : V_GB), g);
+      vst_sel(fwd, V_QF, V_QB, q);
+      vst_sel(fwd, V_PF, V_PB, p);
+      vst_sel(fwd, V_GF, V_GB, g);
       // (no run-time index into the register arrays: that would move them to scratch)
       S(S_VF) = fwd ? S(S_V) : S(S_VF);
       S(S_VB) = fwd ? S(S_VB) : S(S_V);
@@ -911,26 +972,26 @@ struct NutsChain {
       double rho[NCH], psp[NCH], psm[NCH], rho_old[NCH];
       if constexpr (FM) {   // branch-free: the sample point rewritten with a select (LDS image)
         double o_q[NCH], o_g[NCH], nq[NCH], ng[NCH];
-        ld(vp(V_QS), o_q);
-        ld(vp(V_GS), o_g);
-        ld(vp(V_RHO), rho);
+        vld(V_QS, o_q);
+        vld(V_GS, o_g);
+        vld(V_RHO, rho);
 #pragma unroll
         for (int k = 0; k < NCH; ++k) {
           nq[k] = take ? c_q[k] : o_q[k];
           ng[k] = take ? c_g[k] : o_g[k];
         }
-        st(vp(V_QS), nq);
-        st(vp(V_GS), ng);
+        vst(V_QS, nq);
+        vst(V_GS, ng);
         S(S_VS) = take ? c_V : S(S_VS);
         S(S_HS) = take ? c_H : S(S_HS);
       } else {
         if (take) {
-          st(vp(V_QS), c_q);
-          st(vp(V_GS), c_g);
+          vst(V_QS, c_q);
+          vst(V_GS, c_g);
           S(S_VS) = c_V;
           S(S_HS) = c_H;
         }
-        ld(vp(V_RHO), rho);
+        vld(V_RHO, rho);
       }
       S(S_LSW) = lsw_new;
 #pragma unroll
@@ -938,26 +999,26 @@ struct NutsChain {
         rho_old[k] = rho[k];
         rho[k] = rho[k] + c_rho[k];
       }
-      st(vp(V_RHO), rho);
+      vst(V_RHO, rho);
       if constexpr (FM) {   // the end this sub-tree extends gets its p_sharp; the other end's is read
         double oth[NCH];
-        st(vp(fwd ? V_PSP : V_PSM), c_pse);
-        ld(vp(fwd ? V_PSM : V_PSP), oth);
+        vst_sel(fwd, V_PSP, V_PSM, c_pse);
+        vld_sel(fwd, V_PSM, V_PSP, oth);
 #pragma unroll
         for (int k = 0; k < NCH; ++k) {
           psp[k] = fwd ? c_pse[k] : oth[k];
           psm[k] = fwd ? oth[k] : c_pse[k];
         }
       } else if (fwd) {
-        st(vp(V_PSP), c_pse);
+        vst(V_PSP, c_pse);
 #pragma unroll
         for (int k = 0; k < NCH; ++k) psp[k] = c_pse[k];
-        ld(vp(V_PSM), psm);
+        vld(V_PSM, psm);
       } else {
-        st(vp(V_PSM), c_pse);
+        vst(V_PSM, c_pse);
 #pragma unroll
         for (int k = 0; k < NCH; ++k) psm[k] = c_pse[k];
-        ld(vp(V_PSP), psp);
+        vld(V_PSP, psp);
       }
       bool junction_ok = true;
       if (uext()) {
@@ -988,8 +1049,8 @@ struct NutsChain {
         S(S_V) = -lp;
 #pragma unroll
         for (int k = 0; k < NCH; ++k) g[k] = -glp[k];
-        st(vp(V_QS), q);
-        st(vp(V_GS), g);
+        vst(V_QS, q);
+        vst(V_GS, g);
         S(S_VS) = S(S_V);
         IV(I_SSREASON) = 0;
         if (!A.skip_ss && start_probe()) return true;
@@ -1093,11 +1154,12 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   const size_t nv = (size_t)V_COUNT * dpk, ns = (size_t)A.max_depth * stack_vecs(A) * dpk;
   const size_t nss = (size_t)A.max_depth * SS_COUNT;
   constexpr size_t nsc = S_COUNT + (I_COUNT + 1) / 2;   // the chain's scalars and counters
-  const size_t per = (nv + ns + nss + nsc + 2 * SEG + 1) & ~(size_t)1;   // per-chain image + uniform window, even
+  const size_t nvl = ZP ? 0 : nv;                        // ZP: the vectors are in registers (NutsChain::RV)
+  const size_t per = (nvl + ns + nss + nsc + 2 * SEG + 1) & ~(size_t)1;   // per-chain image + uniform window, even
   double* const fl = fl_all + (size_t)seg * per;
   double* const mtab = fl_all + (size_t)CPW * per;                   // exp / log1p table (MT_N doubles)
   mt_init(mtab, (int)threadIdx.x, WAVE);
-  double* const lsc = fl + nv + ns + nss;
+  double* const lsc = fl + nvl + ns + nss;
   int* const liv = (int*)(lsc + S_COUNT);
   double* const gvec = A.vec + (size_t)gid * nv;
   double* const gstk = A.stk + (size_t)gid * A.max_depth * SV_COUNT * A.Dp;   // (allocation stride; ns used)
@@ -1108,18 +1170,19 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
     run = !(mode0 == M_DONE || mode0 == M_ERROR);
   }
   if (run) {
-    for (size_t i = lane; i < nv; i += SEG) fl[i] = gvec[i];
-    for (size_t i = lane; i < ns; i += SEG) fl[nv + i] = gstk[i];
-    for (size_t i = lane; i < nss; i += SEG) fl[nv + ns + i] = gstks[i];
+    for (size_t i = lane; i < nvl; i += SEG) fl[i] = gvec[i];
+    for (size_t i = lane; i < ns; i += SEG) fl[nvl + i] = gstk[i];
+    for (size_t i = lane; i < nss; i += SEG) fl[nvl + ns + i] = gstks[i];
     for (int i = lane; i < S_COUNT; i += SEG) lsc[i] = A.sc[(size_t)gid * S_COUNT + i];
     for (int i = lane; i < I_COUNT; i += SEG) liv[i] = A.iv[(size_t)gid * I_COUNT + i];
   }
   __syncthreads();
   if (run) {
-    NutsChain<NCH, SEG, true, UT, ZP> ch(A, gid, lane, fl, fl + nv, fl + nv + ns, lsc, liv);
+    NutsChain<NCH, SEG, true, UT, ZP> ch(A, gid, lane, fl, fl + nvl, fl + nvl + ns, lsc, liv);
     ch.mt = mtab;
     ch.mk = mt_consts();
-    ch.ub = fl + ((nv + ns + nss + nsc + 1) & ~(size_t)1);   // after the chain's image, 16-B aligned: 2 SEG doubles
+    ch.ub = fl + ((nvl + ns + nss + nsc + 1) & ~(size_t)1);   // after the chain's image, 16-B aligned: 2 SEG doubles
+    ch.rv_in(gvec);
     ch.load();
     ch.fill_uniforms(ch.IV(I_UK) & ~1);                // the current transition's window (a resumed chain)
     double yc[NCH], isc[NCH];
@@ -1149,6 +1212,7 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
         if (req) ++ngrad;
       }
       ch.save();
+      ch.rv_out(gvec);
       ch.flush_counts();
       if (req) ch.st(A.qeval + (size_t)gid * A.Dp, ch.q);
       if (lane == 0) A.cnt[(size_t)gid * C_COUNT + C_GRAD] += ngrad;
@@ -1158,9 +1222,9 @@ __global__ __launch_bounds__(64, MINW) void k_nuts_fused_schools(NutsArgs A, int
   }
   __syncthreads();
   if (run) {
-    for (size_t i = lane; i < nv; i += SEG) gvec[i] = fl[i];
-    for (size_t i = lane; i < ns; i += SEG) gstk[i] = fl[nv + i];
-    for (size_t i = lane; i < nss; i += SEG) gstks[i] = fl[nv + ns + i];
+    for (size_t i = lane; i < nvl; i += SEG) gvec[i] = fl[i];
+    for (size_t i = lane; i < ns; i += SEG) gstk[i] = fl[nvl + i];
+    for (size_t i = lane; i < nss; i += SEG) gstks[i] = fl[nvl + ns + i];
     for (int i = lane; i < S_COUNT; i += SEG)
       if (NutsChain<NCH, SEG>::cold_s(i)) A.sc[(size_t)gid * S_COUNT + i] = lsc[i];
     for (int i = lane; i < I_COUNT; i += SEG)
@@ -1204,7 +1268,8 @@ static hipError_t launch_step_t(const NutsArgs& A, int step_id, int pause_at, hi
 template <int NCH, int CPW, int MINW = 1, int UT = 0, bool ZP = false>
 static hipError_t launch_fused_zp(const NutsArgs& A, int pause_at, int max_steps, hipStream_t st) {
   constexpr int SEG = WAVE / CPW;
-  size_t per = (size_t)V_COUNT * A.Dp + (size_t)A.max_depth * stack_vecs(A) * A.Dp + (size_t)A.max_depth * SS_COUNT +
+  size_t per = (ZP ? 0 : (size_t)V_COUNT * A.Dp) +   // ZP: the vectors are in registers (NutsChain::RV)
+               (size_t)A.max_depth * stack_vecs(A) * A.Dp + (size_t)A.max_depth * SS_COUNT +
                S_COUNT + (I_COUNT + 1) / 2 + 2 * SEG;  // + the chain's uniform window
   per += per & 1;                                        // keep the table after the chains 16-B aligned
   const size_t lds = sizeof(double) * (CPW * per + MT_N);
