@@ -8,6 +8,7 @@ each workload reports whether the arms' results are bit-identical.
                        identical = posterior means, min ESS, divergences, leapfrogs agree
              sweep16   bench.py --throughput-only (configs[3]: 8 x 1.25e7 rows, d = 100, 16
                        chains): k_sweep16's ms per launch (HIP events), identical = grads agree
+             sweep16lin  the same at configs[2]'s shape (linear, 8 x 1.25e6 rows, d = 50)
              fulldata  tools/bench_fulldata.py --steps 6 (configs[4] at 1e7 rows): pass F + B ms
 
 usage: tools/lib_ab.py build NAME [--rev REV] [--flags FILE=FLAGS ...]   (here; -> tools/_bin/ab_NAME; no
@@ -66,6 +67,9 @@ def one(arm, work):
         cmd = [sys.executable, os.path.join(ROOT, "tools", "bench_schools.py")]
     elif work == "sweep16":
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--throughput-only", "--steps", "200", "--warmup", "10"]
+    elif work == "sweep16lin":
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--throughput-only", "--family", "linear", "--rows", "1e7",
+               "--d", "50", "--steps", "2000", "--warmup", "50"]
     else:
         cmd = [sys.executable, os.path.join(ROOT, "tools", "bench_fulldata.py"), "--rows-per-gpu", "1e7", "--steps", "6",
                "--warmup", "2"]
@@ -75,7 +79,7 @@ def one(arm, work):
     ln = json.loads(p.stdout.strip().splitlines()[-1])
     if work == "schools":
         return ln["value"] / 1e6, [ln[k] for k in ("posterior_mean_mu_tau", "min_ess", "divergent", "leapfrogs_per_transition")]
-    if work == "sweep16":
+    if work in ("sweep16", "sweep16lin"):
         return ln["roofline"]["avg_launch_ms"], [round(ln["value"] * ln["ms_per_step"])]
     return ln["roofline"]["avg_launch_ms"], [ln.get("chains_sha16_per_rank")]
 
@@ -105,7 +109,7 @@ def main():
     p.add_argument("--rev", default=None)
     p.add_argument("--flags", nargs="*", default=[])
     p.add_argument("--arms", default="")
-    p.add_argument("--work", default="schools", choices=["schools", "sweep16", "fulldata"])
+    p.add_argument("--work", default="schools", choices=["schools", "sweep16", "sweep16lin", "fulldata"])
     p.add_argument("--rounds", type=int, default=3)
     a = p.parse_args()
     if a.cmd == "build":
