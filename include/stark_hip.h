@@ -186,7 +186,9 @@ STK_API int stk_sampler_destroy(stk_sampler* s);
  * on another device -- continues bit for bit as the unsplit run would (the reference has no
  * counterpart: a pystan fit cannot be resumed; SURVEY.md 8 aux "checkpoint/resume").
  * stk_sampler_state_bytes gives the size of the blob; stk_sampler_load_state refuses a blob
- * of another geometry / config (STK_E_ARG) before writing anything. */
+ * of another geometry / config (STK_E_ARG) before writing anything.  The data rows themselves
+ * are not hashed (that would read the whole shard): loading into a model of the same geometry
+ * built from other data is the caller's error and is not detected. */
 STK_API int stk_sampler_state_bytes(stk_sampler* s, int64_t* bytes);
 STK_API int stk_sampler_save_state(stk_sampler* s, void* buf, int64_t bytes);
 STK_API int stk_sampler_load_state(stk_sampler* s, const void* buf, int64_t bytes);
